@@ -1,0 +1,195 @@
+/*
+ * qsmd.h -- C ABI of the MI355X-native linearisability checker.
+ *
+ * Drop-in boundary for ONE function of advancedtelematic/
+ * quickcheck-state-machine-distributed:
+ *
+ *   linearisable :: Eq pid
+ *                => (model -> Either inv resp -> model)      -- transition
+ *                -> (model -> inv -> resp -> Bool)           -- postcondition
+ *                -> model -> History pid inv resp -> Bool
+ *   (src/Linearisability.hs:52-69, exported at :1-7; History at :18)
+ *
+ * The reference has no FFI; its callers are test/Bank.hs:285,
+ * test/TicketDispenser.hs:253 and :320, one call per history.  The binding a
+ * Haskell maintainer adds (`foreign import ccall safe "qsmd_check_batch"`) is
+ * shown in INTEGRATION.md.  Every entry point below is plain C: caller-owned
+ * buffers, plain pointers and sizes, no C++ or torch types.
+ *
+ * Semantics are bit-exact with the reference search:
+ *   - same verdict for every history;
+ *   - `nodes` = number of `step` evaluations (src/Linearisability.hs:63) of the
+ *     reference's lazy left-to-right short-circuit DFS (exhaustive mode);
+ *   - model exceptions (Bank `Map.!`, test/Bank.hs:128) surface as
+ *     QSMD_STATUS_MODEL_ERROR exactly when the reference would raise them.
+ */
+#ifndef QSMD_H
+#define QSMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QSMD_ABI_VERSION 1u
+
+/* ---------------------------------------------------------------- layout */
+
+/* One history = one header (16 B) + n_ev events (8 B each) stored
+ * contiguously at events[ev_off .. ev_off + n_ev).  Replaces the boxed list
+ * `[(pid, Either inv resp)]` of src/Linearisability.hs:18. */
+typedef struct qsmd_hdr {
+    uint32_t ev_off;    /* index of the first event in the events array      */
+    uint16_t n_ev;      /* number of events (<= QSMD_MAX_EVENTS)             */
+    uint8_t  n_pid;     /* number of distinct dense pids used (<= 128)       */
+    uint8_t  model_id;  /* QSMD_MODEL_* (must equal the call's model_id)     */
+    uint32_t tag;       /* caller's tag, ignored by the checker              */
+    uint32_t reserved;  /* must be 0                                         */
+} qsmd_hdr;
+
+/* One event.  kp = (kind << 7) | pid with kind 0 = Left inv, 1 = Right resp
+ * (src/Linearisability.hs:18); pid is the dense per-history pid (the
+ * marshaller maps `Eq pid` values to 0..n_pid-1 in order of first use). */
+typedef struct qsmd_event {
+    uint8_t kp;
+    uint8_t code;       /* constructor code, model specific (below)          */
+    uint8_t a;          /* Bank: account (dense, < QSMD_BANK_MAX_ACCOUNTS)   */
+    uint8_t b;          /* Bank Transfer: destination account                */
+    int32_t val;        /* Bank money / Balance; Ticket Number               */
+} qsmd_event;
+
+#define QSMD_EV_RESP      0x80u
+#define QSMD_EV_PID_MASK  0x7Fu
+
+#define QSMD_MAX_EVENTS   128   /* 64 operations (SURVEY.md §8b encode limit) */
+#define QSMD_MAX_PIDS     128
+
+/* ---------------------------------------------------------------- models */
+
+#define QSMD_MODEL_TICKET 1u    /* test/TicketDispenser.hs:51-102          */
+#define QSMD_MODEL_BANK   2u    /* test/Bank.hs:41-131                     */
+
+/* TicketDispenser Request / Response (test/TicketDispenser.hs:51-63) */
+#define QSMD_TICKET_TAKE_TICKET 0u
+#define QSMD_TICKET_RESET       1u
+#define QSMD_TICKET_NUMBER      0u   /* Number Int  (val)                  */
+#define QSMD_TICKET_OK          1u
+
+/* BankRequestF / BankResponse (test/Bank.hs:44-73) */
+#define QSMD_BANK_OPEN_ACCOUNT   0u  /* a                                  */
+#define QSMD_BANK_DEPOSIT        1u  /* a, val = money                     */
+#define QSMD_BANK_WITHDRAW       2u  /* a, val = money                     */
+#define QSMD_BANK_CHECK_BALANCE  3u  /* a                                  */
+#define QSMD_BANK_TRANSFER       4u  /* a = from, val = money, b = to      */
+
+#define QSMD_BANK_ACCOUNT_CREATED        0u
+#define QSMD_BANK_DEPOSIT_MADE           1u
+#define QSMD_BANK_WITHDRAWAL_MADE        2u
+#define QSMD_BANK_TRANSFER_MADE          3u
+#define QSMD_BANK_ACCOUNT_ALREADY_EXISTS 4u
+#define QSMD_BANK_ACCOUNT_DOESNT_EXIST   5u
+#define QSMD_BANK_INSUFFICIENT_FUNDS     6u
+#define QSMD_BANK_BALANCE                7u  /* Balance Money (val)         */
+
+#define QSMD_BANK_MAX_ACCOUNTS 8
+
+/* Initial models (the `model0` argument).  NULL = the reference's initModel:
+ * Nothing (test/TicketDispenser.hs:73-74) / M.empty (test/Bank.hs:86-87). */
+typedef struct qsmd_ticket_model {
+    uint32_t is_just;   /* 0 = Nothing, 1 = Just n                          */
+    uint32_t reserved;
+    int64_t  n;         /* must lie in int32 range                          */
+} qsmd_ticket_model;
+
+typedef struct qsmd_bank_model {
+    uint32_t exists;    /* bit a set <=> account a is a key of the Map      */
+    uint32_t reserved;
+    int64_t  balance[QSMD_BANK_MAX_ACCOUNTS];  /* int32 range; 0 if absent  */
+} qsmd_bank_model;
+
+/* -------------------------------------------------------------- results */
+
+#define QSMD_STATUS_NONLINEARISABLE 0u  /* linearisable ... == False        */
+#define QSMD_STATUS_LINEARISABLE    1u  /* == True                          */
+#define QSMD_STATUS_MODEL_ERROR     2u  /* reference raises (Map.!)         */
+#define QSMD_STATUS_ENCODE_ERROR    3u  /* unknown code, pid/account range, */
+                                        /* > QSMD_MAX_EVENTS, bad model_id  */
+#define QSMD_STATUS_BUDGET          4u  /* max_nodes reached, undecided     */
+#define QSMD_STATUS_SKIPPED         5u  /* QSMD_FLAG_EARLY_EXIT_BATCH       */
+
+#define QSMD_FLAG_EXHAUSTIVE       1u  /* reference search, exact counts    */
+#define QSMD_FLAG_MEMO             2u  /* prune known-failing states        */
+#define QSMD_FLAG_WITNESS          4u  /* fill witness_out                  */
+#define QSMD_FLAG_EARLY_EXIT_BATCH 8u  /* stop at first non-linearisable    */
+
+/* Witness: for a LINEARISABLE history i, witness_out[hdr[i].ev_off + d] is
+ * the (history-local) index of the invocation event chosen at depth d of the
+ * successful path; the list ends at the first 0xFF (or at n_ev).  Replay:
+ * at each step the operation is (pid p of that event, its inv, the first
+ * remaining response of p) -- SURVEY.md §8a Lemma L1.  witness_out has as
+ * many bytes as the events array. */
+#define QSMD_WITNESS_END 0xFFu
+
+typedef struct qsmd_totals {
+    uint64_t checked;           /* histories with a decided status         */
+    uint64_t linearisable;
+    uint64_t nonlinearisable;
+    uint64_t model_errors;
+    uint64_t encode_errors;
+    uint64_t budget;
+    uint64_t skipped;
+    uint64_t nodes;             /* sum of per-history node counts          */
+} qsmd_totals;
+
+/* -------------------------------------------------------------- context */
+
+typedef struct qsmd_ctx qsmd_ctx;
+
+/* Return codes: 0 = ok, < 0 = API / device error (qsmd_last_error). */
+#define QSMD_OK              0
+#define QSMD_ERR_ARG        -1
+#define QSMD_ERR_DEVICE     -2
+#define QSMD_ERR_NOMEM      -3
+#define QSMD_ERR_UNSUPPORTED -4
+
+/* Bind a context to one HIP device (one process per GPU). */
+int  qsmd_open(qsmd_ctx** out, int device);
+void qsmd_close(qsmd_ctx* ctx);
+const char* qsmd_last_error(const qsmd_ctx* ctx);
+uint32_t qsmd_abi_version(void);
+
+/* Check a batch held in HOST memory (the drop-in for one call per history;
+ * n_hist = 1 is valid).  Buffers are copied in and out; the library keeps no
+ * pointer after return.  max_nodes = 0 means unbounded.  nodes_out,
+ * witness_out, totals_out and model0 may be NULL.  Synchronous. */
+int qsmd_check_batch(qsmd_ctx* ctx, uint32_t model_id,
+                     const qsmd_hdr* hdr, uint64_t n_hist,
+                     const qsmd_event* events, uint64_t n_events,
+                     const void* model0, uint32_t flags, uint64_t max_nodes,
+                     uint8_t* status_out, uint64_t* nodes_out,
+                     uint8_t* witness_out, qsmd_totals* totals_out);
+
+/* Same, with every buffer already resident in device memory (HBM) and work
+ * enqueued on `stream` (a hipStream_t, NULL = the context's stream).
+ * totals_dev (device, may be NULL) receives the qsmd_totals of the batch.
+ * Asynchronous: synchronise the stream before reading outputs. */
+int qsmd_check_batch_device(qsmd_ctx* ctx, uint32_t model_id,
+                            const qsmd_hdr* hdr_dev, uint64_t n_hist,
+                            const qsmd_event* events_dev, uint64_t n_events,
+                            const void* model0_host, uint32_t flags,
+                            uint64_t max_nodes,
+                            uint8_t* status_dev, uint64_t* nodes_dev,
+                            uint8_t* witness_dev, qsmd_totals* totals_dev,
+                            void* stream);
+
+/* Device time (ms, HIP events on the launch stream) of the search kernels of
+ * the most recent check call, measured once that stream has completed. */
+int qsmd_last_kernel_ms(qsmd_ctx* ctx, float* ms_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* QSMD_H */
