@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark: histories checked per second (and search nodes per second) for
+BASELINE.json config 2 -- 1M synthetic 4-client x 16-op Bank histories per GPU
+(weak scaling: every rank checks its own 1M-history shard of one global
+stream; the histories are independent).
+
+One step = one full pass of the hot path (the linearisability search,
+src/Linearisability.hs:52-69) over the resident batch + the RCCL all-reduce of
+the verdict/node counters (the only collective).  Inputs are resident in HBM
+before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Rank 0 prints one JSON line.  The cpu_baseline leg (N=1, rank 0) times the C
+oracle (oracle/ref_cpu.c, the reference restated with the same semantics) on a
+bounded sample of the same batch on the host's cores.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "quickcheck-state-machine-distributed_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (first: our library shares torch's HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+from qsmd import device, gen  # noqa: E402
+
+METRIC = ("histories checked/sec (whole node) + search nodes/sec, "
+          "4×16-op Bank, 1/2/4/8 GPU")
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def alg_bytes(hdr, nodes):
+    """SURVEY.md §8d algorithmic bytes: per history 16 B header + 16 B per
+    operation (2 events x 8 B) + 16 B result + 16 B per explored node."""
+    n_ev = hdr["n_ev"].astype(np.int64)
+    return int((16 + 8 * n_ev + 16).sum() + 16 * nodes.astype(np.int64).sum())
+
+
+def hbm_bytes(hdr):
+    """Bytes that must cross HBM: header + events in, status + nodes out."""
+    return int((16 + 8 * hdr["n_ev"].astype(np.int64) + 1 + 8).sum())
+
+
+def cpu_baseline(hdr, ev, model_id, target_s):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_c
+    oracle_c.lib()
+    cal = min(len(hdr), 20000)
+    t = time.perf_counter()
+    oracle_c.check_batch(model_id, hdr[:cal], ev, threads=1)
+    dt = time.perf_counter() - t
+    rate = cal / max(dt, 1e-9)
+    sample = int(min(len(hdr), max(cal, rate * target_s)))
+    t = time.perf_counter()
+    st, nd, _ = oracle_c.check_batch(model_id, hdr[:sample], ev, threads=1)
+    dt = time.perf_counter() - t
+    return {"value": sample / dt, "unit": "histories/s", "cores": 1, "kind": "port",
+            "sample": f"first {sample} histories of the rank-0 batch, 1 thread, "
+                      f"{dt:.1f} s, oracle/ref_cpu.c -O3 (reference semantics, no memo)",
+            "nodes_per_sec": float(nd.astype(np.float64).sum() / dt)}, st, nd, sample
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="bank_4x16", choices=sorted(gen.CONFIGS))
+    ap.add_argument("--n-hist", type=int, default=1_000_000, help="histories per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="PMC summary written by profiles/profile.sh (for roofline.traffic)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = dict(gen.CONFIGS[args.config])
+    model_id = cfg["model_id"]
+    n = args.n_hist
+    t = time.perf_counter()
+    hdr, ev, bug = gen.generate(gen.params(**cfg), rank * n, n, threads=min(16, os.cpu_count() or 1))
+    log(f"[rank {rank}] generated {n} histories in {time.perf_counter() - t:.1f}s")
+
+    ctx = device.Context(local)
+    d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
+    d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
+    d_st = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_nd = torch.empty(n, dtype=torch.int64, device=dev)
+    d_tot = torch.zeros(8, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ctx.check_device(model_id, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st.data_ptr(),
+                         d_nd.data_ptr(), None, d_tot.data_ptr(), stream=stream.cuda_stream)
+        if world > 1:
+            dist.all_reduce(d_tot, op=dist.ReduceOp.SUM)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ctx.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    s0_ms, call_ms = ctx.timing_read()
+    st = d_st.cpu().numpy()
+    nd = d_nd.cpu().numpy()
+    tot = d_tot.cpu().numpy()               # global totals of the last step
+    ms_per_step = elapsed / args.steps * 1e3
+    total_hist = n * world
+    value = total_hist * args.steps / elapsed
+    nodes_total = int(tot[7])
+    assert int(tot[0]) + int(tot[4]) + int(tot[5]) == total_hist, tot
+
+    # roofline of the dominant kernel (stage 0 search), rank-local
+    s0_mean = float(np.mean(s0_ms)) if len(s0_ms) else float("nan")
+    a_bytes = alg_bytes(hdr, nd)
+    achieved = a_bytes / (s0_mean * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic):
+        with open(args.traffic) as f:
+            tr = json.load(f)
+        if tr.get("config") == args.config and tr.get("n_hist") == n:
+            traffic = tr.get("hbm_bytes_per_launch")
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "histories/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (seeded scheduler-policy generator, include/qsmd_gen.h)",
+        "config": {"workload": args.config, "histories_per_gpu": n,
+                   "clients": cfg["n_clients"], "ops": cfg["n_ops"],
+                   "events_per_history": 2 * cfg["n_ops"], "parallelism": f"shard{world}",
+                   "mode": "exhaustive"},
+        "nodes_per_sec": nodes_total * args.steps / elapsed,
+        "verdicts": {"checked": int(tot[0]), "linearisable": int(tot[1]),
+                     "nonlinearisable": int(tot[2]), "model_errors": int(tot[3]),
+                     "budget": int(tot[5])},
+        "device_ms": {"stage0_mean": s0_mean, "call_mean": float(np.mean(call_ms)) if len(call_ms) else None},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "alg_bytes_per_launch": a_bytes, "hbm_io_bytes_per_launch": hbm_bytes(hdr),
+                     "kernel": "lane_search<Bank,u32,32,8,64> (stage 0)"},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb, st_o, nd_o, sample = cpu_baseline(hdr, ev, model_id, args.cpu_seconds)
+        out["cpu_baseline"] = cb
+        out["mismatches_vs_oracle"] = int(((st_o != st[:sample]) | (nd_o != nd[:sample].astype(np.uint64))).sum())
+        out["checked_vs_oracle"] = sample
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

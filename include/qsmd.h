@@ -184,9 +184,21 @@ int qsmd_check_batch_device(qsmd_ctx* ctx, uint32_t model_id,
                             uint8_t* witness_dev, qsmd_totals* totals_dev,
                             void* stream);
 
+/* Safety net: a search launch whose lanes run longer than this wall time
+ * stops and reports QSMD_STATUS_BUDGET for the unfinished histories (default
+ * 120000 ms; 0 disables).  Not part of the reference semantics. */
+int qsmd_set_time_limit_ms(qsmd_ctx* ctx, uint64_t ms);
+
 /* Device time (ms, HIP events on the launch stream) of the search kernels of
  * the most recent check call, measured once that stream has completed. */
 int qsmd_last_kernel_ms(qsmd_ctx* ctx, float* ms_out);
+
+/* Per-call device timings since the last reset (at most the last 1024 calls):
+ * stage0_ms[i] = the first (dominant) search kernel, call_ms[i] = every
+ * kernel of call i.  Synchronises on the recorded events. */
+int qsmd_timing_reset(qsmd_ctx* ctx);
+int qsmd_timing_read(qsmd_ctx* ctx, float* stage0_ms, float* call_ms, uint64_t max,
+                     uint64_t* n_out);
 
 #ifdef __cplusplus
 }

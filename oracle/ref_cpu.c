@@ -161,6 +161,7 @@ static void ticket_next(ticket_m* m, const qsmd_event* inv) {
 static int valid_history(uint32_t model_id, const qsmd_hdr* h, const qsmd_event* ev) {
     if (h->model_id != model_id) return 0;
     if (h->n_ev > QSMD_MAX_EVENTS) return 0;
+    if (h->n_pid > QSMD_MAX_PIDS) return 0;
     for (int e = 0; e < h->n_ev; ++e) {
         const qsmd_event* x = &ev[e];
         int pid = x->kp & QSMD_EV_PID_MASK;

@@ -1,0 +1,322 @@
+// api.hip -- the C ABI of include/qsmd.h: context, workspace, stage cascade.
+//
+// Replaces the call `linearisable transition postcondition model0 hist`
+// (src/Linearisability.hs:52-69) made once per history at test/Bank.hs:285,
+// test/TicketDispenser.hs:253 and :320 with one batched call.  The model
+// closures are selected by model_id (device functors, csrc/models.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+#include "qsmd.h"
+
+using namespace qsmd;
+
+struct qsmd_ctx {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::string err;
+    // workspace (device)
+    char* ws = nullptr;
+    size_t ws_bytes = 0;
+    // staging for the host-memory entry point (device)
+    char* io = nullptr;
+    size_t io_bytes = 0;
+    // timing: per call, events before stage 0, after stage 0 and after the
+    // final reduction, recorded on the launch stream (a ring of kTimingSlots)
+    std::vector<hipEvent_t> ev;          // 3 per slot
+    uint64_t n_calls = 0;                // calls recorded since the last reset
+    bool timed = false;
+    uint64_t time_limit_ms = 120000;   // safety net per search launch
+};
+
+namespace {
+
+constexpr uint32_t kStage1Grid = 1024;   // list-mode stages: grid-stride
+constexpr uint32_t kStage2Grid = 1024;
+constexpr uint64_t kStage0MaxGrid = 65536;
+constexpr uint64_t kTimingSlots = 1024;
+
+int fail(qsmd_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
+    if (c) {
+        char buf[256];
+        if (e != hipSuccess) std::snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+        else std::snprintf(buf, sizeof buf, "%s", what);
+        c->err = buf;
+    }
+    return code;
+}
+
+#define HIP_TRY(c, expr, what)                                  \
+    do {                                                        \
+        hipError_t _e = (expr);                                 \
+        if (_e != hipSuccess) return fail((c), QSMD_ERR_DEVICE, (what), _e); \
+    } while (0)
+
+size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
+
+int grow(qsmd_ctx* c, char** buf, size_t* cap, size_t need) {
+    if (*cap >= need) return QSMD_OK;
+    if (*buf) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(*buf);
+        *buf = nullptr;
+        *cap = 0;
+    }
+    size_t sz = std::max(need, *cap * 3 / 2);
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(buf), sz);
+    if (e != hipSuccess) return fail(c, QSMD_ERR_NOMEM, "hipMalloc", e);
+    *cap = sz;
+    return QSMD_OK;
+}
+
+bool in_i32(int64_t v) { return v >= INT32_MIN && v <= INT32_MAX; }
+
+int fill_model0(qsmd_ctx* c, uint32_t model_id, const void* model0, SearchArgs& a) {
+    a.m0_exists = 0;
+    a.m0_just = 0;
+    for (auto& v : a.m0_val) v = 0;
+    if (!model0) return QSMD_OK;
+    if (model_id == QSMD_MODEL_BANK) {
+        const auto* m = static_cast<const qsmd_bank_model*>(model0);
+        if (m->exists >> QSMD_BANK_MAX_ACCOUNTS) return fail(c, QSMD_ERR_ARG, "model0: account >= 8");
+        for (int i = 0; i < QSMD_BANK_MAX_ACCOUNTS; ++i) {
+            const bool ex = (m->exists >> i) & 1u;
+            if (!in_i32(m->balance[i]) || (!ex && m->balance[i] != 0))
+                return fail(c, QSMD_ERR_ARG, "model0: balance outside int32 or set on an absent account");
+            a.m0_val[i] = m->balance[i];
+        }
+        a.m0_exists = m->exists;
+    } else {
+        const auto* m = static_cast<const qsmd_ticket_model*>(model0);
+        if (m->is_just > 1 || !in_i32(m->n)) return fail(c, QSMD_ERR_ARG, "model0: bad Maybe Int");
+        a.m0_just = m->is_just;
+        a.m0_val[0] = m->is_just ? m->n : 0;
+    }
+    return QSMD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t qsmd_abi_version(void) { return QSMD_ABI_VERSION; }
+
+const char* qsmd_last_error(const qsmd_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int qsmd_open(qsmd_ctx** out, int device) {
+    if (!out) return QSMD_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return QSMD_ERR_DEVICE;
+    if (device < 0 || device >= n) return QSMD_ERR_ARG;
+    auto* c = new qsmd_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return QSMD_ERR_DEVICE;
+    }
+    c->ev.resize(3 * kTimingSlots, nullptr);
+    for (auto& e : c->ev) {
+        if (hipEventCreate(&e) != hipSuccess) { qsmd_close(c); return QSMD_ERR_DEVICE; }
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+    *out = c;
+    return QSMD_OK;
+}
+
+void qsmd_close(qsmd_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->io) (void)hipFree(c->io);
+    for (auto e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int qsmd_set_time_limit_ms(qsmd_ctx* c, uint64_t ms) {
+    if (!c) return QSMD_ERR_ARG;
+    c->time_limit_ms = ms;
+    return QSMD_OK;
+}
+
+static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, uint64_t n_hist,
+                               const qsmd_event* events, uint64_t n_events, const void* model0,
+                               uint32_t flags, uint64_t max_nodes, uint8_t* status, uint64_t* nodes,
+                               uint8_t* witness, qsmd_totals* totals, hipStream_t s) {
+    if (model_id != QSMD_MODEL_BANK && model_id != QSMD_MODEL_TICKET)
+        return fail(c, QSMD_ERR_ARG, "unknown model_id");
+    if (n_hist && (!hdr || !status)) return fail(c, QSMD_ERR_ARG, "null hdr/status");
+    if (n_hist > 0xFFFFFFFFull) return fail(c, QSMD_ERR_ARG, "n_hist > 2^32-1");
+    if (flags & QSMD_FLAG_EARLY_EXIT_BATCH)
+        return fail(c, QSMD_ERR_UNSUPPORTED, "EARLY_EXIT_BATCH not implemented yet");
+    SearchArgs a{};
+    int rc = fill_model0(c, model_id, model0, a);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+
+    // ---- workspace: defer lists, counters, partials, internal totals
+    const uint64_t g0 = std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), kStage0MaxGrid);
+    const uint64_t n_part = g0 + kStage1Grid + kStage2Grid;
+    const size_t off_cnt = 0;                                          // 4 x u32
+    const size_t off_tot = 256;                                        // qsmd_totals
+    const size_t off_l0 = 512;
+    const size_t off_l1 = off_l0 + align_up(n_hist * 4 + 4);
+    const size_t off_part = off_l1 + align_up(n_hist * 4 + 4);
+    const size_t need = off_part + align_up(n_part * T_N * 8);
+    rc = grow(c, &c->ws, &c->ws_bytes, need);
+    if (rc) return rc;
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(c->ws + off_cnt);
+    qsmd_totals* tot = totals ? totals : reinterpret_cast<qsmd_totals*>(c->ws + off_tot);
+    uint32_t* l0 = reinterpret_cast<uint32_t*>(c->ws + off_l0);
+    uint32_t* l1 = reinterpret_cast<uint32_t*>(c->ws + off_l1);
+    unsigned long long* part = reinterpret_cast<unsigned long long*>(c->ws + off_part);
+
+    HIP_TRY(c, hipMemsetAsync(cnt, 0, 16, s), "memset counters");
+    HIP_TRY(c, hipMemsetAsync(tot, 0, sizeof(qsmd_totals), s), "memset totals");
+
+    a.hdr = hdr;
+    a.events = reinterpret_cast<const uint2*>(events);
+    a.n_hist = n_hist;
+    a.n_events = n_events;
+    a.flags = flags;
+    a.model_id = model_id;
+    a.max_nodes = max_nodes;
+    a.time_limit = c->time_limit_ms * 100000ull;   // 100 MHz s_memrealtime
+    a.status = status;
+    a.nodes = nodes;
+    a.witness = (flags & QSMD_FLAG_WITNESS) ? witness : nullptr;
+    a.timed_out = cnt + 2;
+
+    hipEvent_t* evs = &c->ev[3 * (c->n_calls % kTimingSlots)];
+    HIP_TRY(c, hipEventRecord(evs[0], s), "hipEventRecord");
+    // stage 0: direct over [0, n_hist)
+    SearchArgs a0 = a;
+    a0.list = nullptr;
+    a0.list_count = nullptr;
+    a0.defer_list = l0;
+    a0.defer_count = cnt + 0;
+    a0.partials = part;
+    HIP_TRY(c, launch_stage(0, a0, (uint32_t)g0, s), "stage 0 launch");
+    HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
+    // stage 1: histories with 33..64 events
+    SearchArgs a1 = a;
+    a1.list = l0;
+    a1.list_count = cnt + 0;
+    a1.defer_list = l1;
+    a1.defer_count = cnt + 1;
+    a1.partials = part + g0 * T_N;
+    HIP_TRY(c, launch_stage(1, a1, kStage1Grid, s), "stage 1 launch");
+    // stage 2: up to 128 events / 128 pids
+    SearchArgs a2 = a;
+    a2.list = l1;
+    a2.list_count = cnt + 1;
+    a2.defer_list = l0;            // never written: stage 2 holds every valid history
+    a2.defer_count = cnt + 3;
+    a2.partials = part + (g0 + kStage1Grid) * T_N;
+    HIP_TRY(c, launch_stage(2, a2, kStage2Grid, s), "stage 2 launch");
+    HIP_TRY(c, launch_reduce(part, n_part, tot, s), "reduce launch");
+    HIP_TRY(c, hipEventRecord(evs[2], s), "hipEventRecord");
+    c->n_calls++;
+    c->timed = true;
+    return QSMD_OK;
+}
+
+int qsmd_check_batch_device(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr_dev, uint64_t n_hist,
+                            const qsmd_event* events_dev, uint64_t n_events, const void* model0_host,
+                            uint32_t flags, uint64_t max_nodes, uint8_t* status_dev, uint64_t* nodes_dev,
+                            uint8_t* witness_dev, qsmd_totals* totals_dev, void* stream) {
+    if (!c) return QSMD_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    return check_device_locked(c, model_id, hdr_dev, n_hist, events_dev, n_events, model0_host, flags,
+                               max_nodes, status_dev, nodes_dev, witness_dev, totals_dev, s);
+}
+
+int qsmd_check_batch(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, uint64_t n_hist,
+                     const qsmd_event* events, uint64_t n_events, const void* model0, uint32_t flags,
+                     uint64_t max_nodes, uint8_t* status_out, uint64_t* nodes_out, uint8_t* witness_out,
+                     qsmd_totals* totals_out) {
+    if (!c) return QSMD_ERR_ARG;
+    if (n_hist && (!hdr || !status_out)) return fail(c, QSMD_ERR_ARG, "null hdr/status");
+    if (n_events && !events) return fail(c, QSMD_ERR_ARG, "null events");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    hipStream_t s = c->stream;
+    const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness_out;
+    const size_t o_hdr = 0;
+    const size_t o_ev = o_hdr + align_up(n_hist * sizeof(qsmd_hdr));
+    const size_t o_st = o_ev + align_up(n_events * sizeof(qsmd_event));
+    const size_t o_nd = o_st + align_up(n_hist);
+    const size_t o_w = o_nd + align_up(n_hist * 8);
+    const size_t o_tot = o_w + align_up(want_w ? n_events : 0);
+    const size_t need = o_tot + align_up(sizeof(qsmd_totals));
+    int rc = grow(c, &c->io, &c->io_bytes, need);
+    if (rc) return rc;
+    auto* d_hdr = reinterpret_cast<qsmd_hdr*>(c->io + o_hdr);
+    auto* d_ev = reinterpret_cast<qsmd_event*>(c->io + o_ev);
+    auto* d_st = reinterpret_cast<uint8_t*>(c->io + o_st);
+    auto* d_nd = reinterpret_cast<uint64_t*>(c->io + o_nd);
+    auto* d_w = reinterpret_cast<uint8_t*>(c->io + o_w);
+    auto* d_tot = reinterpret_cast<qsmd_totals*>(c->io + o_tot);
+    if (n_hist) HIP_TRY(c, hipMemcpyAsync(d_hdr, hdr, n_hist * sizeof(qsmd_hdr), hipMemcpyHostToDevice, s), "H2D hdr");
+    if (n_events) HIP_TRY(c, hipMemcpyAsync(d_ev, events, n_events * sizeof(qsmd_event), hipMemcpyHostToDevice, s), "H2D events");
+    if (want_w) HIP_TRY(c, hipMemsetAsync(d_w, 0xFF, n_events, s), "memset witness");
+    rc = check_device_locked(c, model_id, d_hdr, n_hist, d_ev, n_events, model0, flags, max_nodes, d_st, d_nd,
+                             want_w ? d_w : nullptr, d_tot, s);
+    if (rc) return rc;
+    if (n_hist) HIP_TRY(c, hipMemcpyAsync(status_out, d_st, n_hist, hipMemcpyDeviceToHost, s), "D2H status");
+    if (n_hist && nodes_out) HIP_TRY(c, hipMemcpyAsync(nodes_out, d_nd, n_hist * 8, hipMemcpyDeviceToHost, s), "D2H nodes");
+    if (want_w) HIP_TRY(c, hipMemcpyAsync(witness_out, d_w, n_events, hipMemcpyDeviceToHost, s), "D2H witness");
+    qsmd_totals t{};
+    HIP_TRY(c, hipMemcpyAsync(&t, d_tot, sizeof t, hipMemcpyDeviceToHost, s), "D2H totals");
+    HIP_TRY(c, hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (totals_out) *totals_out = t;
+    return QSMD_OK;
+}
+
+int qsmd_last_kernel_ms(qsmd_ctx* c, float* ms) {
+    if (!c || !ms) return QSMD_ERR_ARG;
+    if (!c->timed || c->n_calls == 0) return fail(c, QSMD_ERR_ARG, "no check call yet");
+    hipEvent_t* evs = &c->ev[3 * ((c->n_calls - 1) % kTimingSlots)];
+    HIP_TRY(c, hipEventSynchronize(evs[2]), "hipEventSynchronize");
+    HIP_TRY(c, hipEventElapsedTime(ms, evs[0], evs[2]), "hipEventElapsedTime");
+    return QSMD_OK;
+}
+
+int qsmd_timing_reset(qsmd_ctx* c) {
+    if (!c) return QSMD_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->n_calls = 0;
+    return QSMD_OK;
+}
+
+int qsmd_timing_read(qsmd_ctx* c, float* stage0_ms, float* call_ms, uint64_t max, uint64_t* n_out) {
+    if (!c || !n_out) return QSMD_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(c->n_calls, kTimingSlots), max);
+    const uint64_t first = c->n_calls - n;
+    for (uint64_t i = 0; i < n; ++i) {
+        hipEvent_t* evs = &c->ev[3 * ((first + i) % kTimingSlots)];
+        HIP_TRY(c, hipEventSynchronize(evs[2]), "hipEventSynchronize");
+        if (stage0_ms) HIP_TRY(c, hipEventElapsedTime(&stage0_ms[i], evs[0], evs[1]), "elapsed");
+        if (call_ms) HIP_TRY(c, hipEventElapsedTime(&call_ms[i], evs[0], evs[2]), "elapsed");
+    }
+    *n_out = n;
+    return QSMD_OK;
+}
+
+}  // extern "C"

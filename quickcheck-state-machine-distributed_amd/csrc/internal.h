@@ -1,0 +1,51 @@
+// internal.h -- declarations shared by the search kernels and the C-ABI host.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "qsmd.h"
+
+namespace qsmd {
+
+// Per-block partial totals, reduced into qsmd_totals by reduce_totals().
+enum { T_CHECKED = 0, T_LIN, T_NONLIN, T_ERR, T_ENC, T_BUDGET, T_SKIPPED, T_NODES, T_N };
+
+// Everything one search launch needs (passed by value).
+struct SearchArgs {
+    const qsmd_hdr* hdr;
+    const uint2* events;          // qsmd_event viewed as {lo word, val}
+    uint64_t n_hist;
+    uint64_t n_events;            // bound for every ev_off + n_ev
+    // list mode: histories are list[0 .. *list_count), else 0 .. n_hist
+    const uint32_t* list;
+    const uint32_t* list_count;
+    // overflow: histories this stage cannot hold go to defer_list
+    uint32_t* defer_list;
+    uint32_t* defer_count;
+    uint32_t flags;
+    uint32_t model_id;
+    uint64_t max_nodes;           // 0 = unbounded
+    uint64_t time_limit;          // s_memrealtime ticks (100 MHz), 0 = none
+    // initial model (model0): Bank exists + balances / Ticket just + n (val[0])
+    uint32_t m0_exists;
+    uint32_t m0_just;
+    int64_t m0_val[QSMD_BANK_MAX_ACCOUNTS];
+    // outputs
+    uint8_t* status;
+    uint64_t* nodes;              // may be null
+    uint8_t* witness;             // may be null
+    unsigned long long* partials; // [gridDim.x][T_N]
+    uint32_t* timed_out;          // set to 1 if the time limit fired
+};
+
+// Stage kernels: each returns the number of blocks it launched (for the
+// partials buffer layout) through *blocks.
+hipError_t launch_stage(int stage, const SearchArgs& a, uint32_t grid, hipStream_t s);
+uint32_t stage_lanes(int stage);
+uint32_t stage_max_events(int stage);
+
+hipError_t launch_reduce(const unsigned long long* partials, uint64_t n_blocks,
+                         qsmd_totals* totals, hipStream_t s);
+
+}  // namespace qsmd

@@ -1,0 +1,179 @@
+"""ctypes binding of the C ABI (include/qsmd.h) -> lib/libqsmd.so.
+
+This is the product path: there is no CPU fallback.  If the HIP library is
+missing or no GPU is visible, every entry point raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import codec
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libqsmd.so")
+
+QSMD_FLAG_EXHAUSTIVE = 1
+QSMD_FLAG_MEMO = 2
+QSMD_FLAG_WITNESS = 4
+QSMD_FLAG_EARLY_EXIT_BATCH = 8
+
+
+class DeviceError(RuntimeError):
+    pass
+
+
+class Totals(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "checked", "linearisable", "nonlinearisable", "model_errors", "encode_errors",
+        "budget", "skipped", "nodes")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+_lib = None
+
+_P = ctypes.c_void_p
+_U32, _U64, _I = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+
+EXPORTS = {
+    "qsmd_abi_version": (_U32, []),
+    "qsmd_open": (_I, [ctypes.POINTER(_P), _I]),
+    "qsmd_close": (None, [_P]),
+    "qsmd_last_error": (ctypes.c_char_p, [_P]),
+    "qsmd_set_time_limit_ms": (_I, [_P, _U64]),
+    "qsmd_check_batch": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P]),
+    "qsmd_check_batch_device": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P, _P]),
+    "qsmd_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
+    "qsmd_timing_reset": (_I, [_P]),
+    "qsmd_timing_read": (_I, [_P, _P, _P, _U64, ctypes.POINTER(_U64)]),
+}
+
+
+def load_library(path=LIB_PATH):
+    """Load lib/libqsmd.so and declare every exported symbol."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise DeviceError(f"{path} not built: run `make -C {PKG_DIR}` (no CPU fallback exists)")
+    # One HIP runtime per process: PyTorch-ROCm bundles its own
+    # libamdhip64.so (SONAME libamdhip64.so.7).  Importing torch first makes
+    # libqsmd.so bind to that same runtime, so torch device memory, streams
+    # and torch.distributed (RCCL) interoperate with our kernels; without
+    # torch the library uses /opt/rocm's runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(arr):
+    return None if arr is None else ctypes.c_void_p(arr.ctypes.data)
+
+
+class Context:
+    """One context per GPU (one process per GPU)."""
+
+    def __init__(self, device=0, time_limit_ms=None):
+        lib = load_library()
+        h = ctypes.c_void_p()
+        rc = lib.qsmd_open(ctypes.byref(h), int(device))
+        if rc != 0:
+            raise DeviceError(f"qsmd_open(device={device}) failed with {rc}: no usable HIP device")
+        self._h = h
+        self._lib = lib
+        if time_limit_ms is not None:
+            lib.qsmd_set_time_limit_ms(h, int(time_limit_ms))
+
+    def close(self):
+        if self._h:
+            self._lib.qsmd_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self._lib.qsmd_last_error(self._h)
+            raise DeviceError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def check_arrays(self, model_id, hdr, events, model0=None, flags=QSMD_FLAG_EXHAUSTIVE,
+                     max_nodes=0, witness=False):
+        """Host-memory batch (numpy arrays in the include/qsmd.h layout).
+        Returns (status u8[n], nodes u64[n], witness u8[n_events] or None, totals dict)."""
+        hdr = np.ascontiguousarray(hdr, dtype=codec.HDR_DTYPE)
+        events = np.ascontiguousarray(events, dtype=codec.EV_DTYPE)
+        n = len(hdr)
+        status = np.empty(n, dtype=np.uint8)
+        nodes = np.empty(n, dtype=np.uint64)
+        wit = np.full(len(events), 0xFF, dtype=np.uint8) if witness else None
+        if witness:
+            flags |= QSMD_FLAG_WITNESS
+        tot = Totals()
+        m0 = ctypes.cast(ctypes.pointer(model0), ctypes.c_void_p) if model0 is not None else None
+        rc = self._lib.qsmd_check_batch(
+            self._h, model_id, _ptr(hdr) if n else None, n,
+            _ptr(events) if len(events) else None, len(events), m0, flags, max_nodes,
+            _ptr(status) if n else None, _ptr(nodes) if n else None,
+            _ptr(wit) if (wit is not None and len(events)) else None, ctypes.byref(tot))
+        self._check(rc, "qsmd_check_batch")
+        return status, nodes, wit, tot.as_dict()
+
+    def check_device(self, model_id, hdr_ptr, n_hist, events_ptr, n_events, status_ptr,
+                     nodes_ptr=None, witness_ptr=None, totals_ptr=None, model0=None,
+                     flags=QSMD_FLAG_EXHAUSTIVE, max_nodes=0, stream=None):
+        """Device-resident batch: raw device pointers (ints), async on stream."""
+        m0 = ctypes.cast(ctypes.pointer(model0), ctypes.c_void_p) if model0 is not None else None
+        rc = self._lib.qsmd_check_batch_device(
+            self._h, model_id, hdr_ptr, n_hist, events_ptr, n_events, m0, flags, max_nodes,
+            status_ptr, nodes_ptr, witness_ptr, totals_ptr, stream)
+        self._check(rc, "qsmd_check_batch_device")
+
+    def last_kernel_ms(self):
+        ms = ctypes.c_float()
+        self._check(self._lib.qsmd_last_kernel_ms(self._h, ctypes.byref(ms)), "qsmd_last_kernel_ms")
+        return float(ms.value)
+
+    def timing_reset(self):
+        self._check(self._lib.qsmd_timing_reset(self._h), "qsmd_timing_reset")
+
+    def timing_read(self, max_calls=1024):
+        """(stage0_ms, call_ms) arrays for the calls since timing_reset()."""
+        s0 = np.zeros(max_calls, dtype=np.float32)
+        call = np.zeros(max_calls, dtype=np.float32)
+        n = ctypes.c_uint64()
+        self._check(self._lib.qsmd_timing_read(self._h, _ptr(s0), _ptr(call), max_calls,
+                                               ctypes.byref(n)), "qsmd_timing_read")
+        return s0[: n.value], call[: n.value]
+
+
+_default = None
+
+
+def default_context():
+    global _default
+    if _default is None:
+        _default = Context(0)
+    return _default

@@ -31,7 +31,7 @@ def bank_event(rng, accounts, vmax=12):
 
 def random_history(rng, model, n_ev, n_pid):
     pids = [f"p{i}" for i in range(n_pid)]
-    accounts = pids[:]
+    accounts = pids[:6]
     h = []
     for _ in range(n_ev):
         p = rng.choice(pids)
@@ -51,9 +51,9 @@ def wellformed_history(rng, model, n_ops, n_pid, p_pending=0.1):
         if pending[p] is None:
             if ops_left == 0:
                 continue
-            ev = ticket_event(rng) if model == "ticket" else bank_event(rng, pids)
+            ev = ticket_event(rng) if model == "ticket" else bank_event(rng, pids[:6])
             while ev[0] != "L":
-                ev = ticket_event(rng) if model == "ticket" else bank_event(rng, pids)
+                ev = ticket_event(rng) if model == "ticket" else bank_event(rng, pids[:6])
             h.append((p, ev))
             pending[p] = ev
             ops_left -= 1
@@ -61,9 +61,9 @@ def wellformed_history(rng, model, n_ops, n_pid, p_pending=0.1):
             if rng.random() < p_pending and ops_left == 0:
                 pending[p] = None          # leave it pending
                 continue
-            ev = ticket_event(rng) if model == "ticket" else bank_event(rng, pids)
+            ev = ticket_event(rng) if model == "ticket" else bank_event(rng, pids[:6])
             while ev[0] != "R":
-                ev = ticket_event(rng) if model == "ticket" else bank_event(rng, pids)
+                ev = ticket_event(rng) if model == "ticket" else bank_event(rng, pids[:6])
             h.append((p, ev))
             pending[p] = None
     return h

@@ -1,0 +1,183 @@
+"""GPU parity: the HIP search (through the C ABI) against the oracle.
+
+Bar: bit-exact verdicts, node counts and witness paths for every history
+(integer search, no tolerance).  Oracles: the C restatement (oracle/ref_cpu.c),
+itself pinned to the literal list transliteration and the KATs
+(tests/test_oracle.py).
+"""
+
+import random
+
+import numpy as np
+import pytest
+
+import histgen
+import oracle_c
+from kats import KATS
+from qsmd import codec, gen, models
+from qsmd.linearisability import linearisable, linearisable_batch, replay_witness
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(ctx, model_id, hdr, events, model0=None, max_nodes=0, threads=8, witness=True):
+    st_d, nd_d, w_d, tot = ctx.check_arrays(model_id, hdr, events, model0, max_nodes=max_nodes,
+                                            witness=witness)
+    st_o, nd_o, w_o = oracle_c.check_batch(model_id, hdr, events, model0, max_nodes, threads,
+                                           witness=witness)
+    bad = np.nonzero((st_d != st_o) | (nd_d != nd_o))[0]
+    assert len(bad) == 0, (f"{len(bad)} mismatches, first {bad[:5]}: "
+                           f"dev {st_d[bad[:5]]}/{nd_d[bad[:5]]} oracle {st_o[bad[:5]]}/{nd_o[bad[:5]]}")
+    if witness:
+        lin = st_d == codec.STATUS_LIN
+        for i in np.nonzero(lin)[0]:
+            h = hdr[i]
+            a, b = int(h["ev_off"]), int(h["ev_off"]) + int(h["n_ev"])
+            assert np.array_equal(w_d[a:b], w_o[a:b]), f"witness mismatch at history {i}"
+    assert tot["nodes"] == int(nd_d.sum())
+    assert tot["linearisable"] == int((st_d == 1).sum())
+    assert tot["nonlinearisable"] == int((st_d == 0).sum())
+    assert tot["model_errors"] == int((st_d == 2).sum())
+    assert tot["encode_errors"] == int((st_d == 3).sum())
+    return st_d, nd_d, w_d
+
+
+def test_kats_on_device(ctx):
+    for name, (m, hist, status, nodes) in KATS.items():
+        res = linearisable_batch(m, [hist], ctx=ctx, witness=True)
+        assert res.verdict(0) == status, name
+        assert int(res.nodes[0]) == nodes, name
+        if status == "lin":
+            assert replay_witness(m, hist, res.witness_of(0)), name
+
+
+def test_linearisable_signature(ctx):
+    """The reference signature: linearisable transition postcondition model0 history."""
+    _, h2, _, _ = KATS["KAT2_reference_example"]
+    _, h3, _, _ = KATS["KAT3_distinct_pids"]
+    T = models.TICKET
+    assert linearisable(T.transition, T.postcondition, T.init_model, h2, ctx=ctx) is False
+    assert linearisable(T.transition, T.postcondition, T.init_model, h3, ctx=ctx) is True
+    _, h8, _, _ = KATS["KAT8_bank_map_error"]
+    B = models.BANK
+    with pytest.raises(models.ModelError):
+        linearisable(B.transition, B.postcondition, B.init_model, h8, ctx=ctx)
+    with pytest.raises(NotImplementedError):
+        linearisable(lambda m, e: m, lambda m, i, r: True, None, h3, ctx=ctx)
+
+
+@pytest.mark.parametrize("model", ["ticket", "bank"])
+def test_random_any_shape(ctx, model):
+    """Ill-formed, shared-pid, pending and stray-response histories."""
+    rng = random.Random(1234 if model == "ticket" else 4321)
+    hs = []
+    for _ in range(6000):
+        if rng.random() < 0.5:
+            hs.append(histgen.random_history(rng, model, rng.randint(0, 16), rng.randint(1, 5)))
+        else:
+            hs.append(histgen.wellformed_history(rng, model, rng.randint(0, 10), rng.randint(1, 5)))
+    m = models.BY_NAME[model]
+    b = codec.encode(m, hs)
+    _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
+
+
+@pytest.mark.parametrize("n_ev,n_pid", [(40, 3), (64, 6), (96, 4), (128, 8), (60, 20), (128, 100)])
+def test_stage_cascade(ctx, n_ev, n_pid):
+    """Histories beyond stage 0 (32 events / 8 pids) go through stages 1 and 2."""
+    rng = random.Random(n_ev * 1000 + n_pid)
+    for model in ("ticket", "bank"):
+        hs = [histgen.wellformed_history(rng, model, n_ev // 2, n_pid, p_pending=0.0)[:n_ev]
+              for _ in range(300)]
+        hs += [histgen.random_history(rng, model, n_ev, n_pid) for _ in range(300)]
+        m = models.BY_NAME[model]
+        b = codec.encode(m, hs)
+        _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
+
+
+def test_mixed_sizes_one_batch(ctx):
+    rng = random.Random(7)
+    hs = []
+    for _ in range(3000):
+        n = rng.choice([0, 1, 2, 8, 20, 32, 33, 50, 64, 65, 100, 128])
+        hs.append(histgen.random_history(rng, "bank", n, rng.randint(1, 12)))
+    b = codec.encode(models.BANK, hs)
+    _compare(ctx, models.MODEL_BANK, b.hdr, b.events, max_nodes=100000)
+
+
+@pytest.mark.parametrize("name,n", [("ticket_2x10", 20000), ("bank_4x16", 50000),
+                                    ("bank_4x16_bugs", 50000), ("bank_6x24", 20000)])
+def test_generated_configs(ctx, name, n):
+    hdr, ev, bug = gen.generate_config(name, 0, n)
+    st, nd, _ = _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+    if name in ("bank_4x16", "bank_6x24"):
+        assert (st == codec.STATUS_LIN).all()
+
+
+def test_model0(ctx):
+    rng = random.Random(99)
+    hs = [histgen.wellformed_history(rng, "ticket", rng.randint(1, 6), 2) for _ in range(2000)]
+    b = codec.encode(models.TICKET, hs)
+    for n0 in (0, 5, -3):
+        _compare(ctx, models.MODEL_TICKET, b.hdr, b.events, models.TicketModel(1, 0, n0))
+    accts = ["p0", "p1", "p2"]
+    model0 = {"p0": 10, "p1": 0, "p2": 3}
+    hs = [histgen.wellformed_history(rng, "bank", rng.randint(1, 6), 3) for _ in range(2000)]
+    b = codec.encode(models.BANK, hs, model0)
+    packed = models.BANK.pack_model0(model0, models.BANK.new_account_map(model0))
+    assert packed.exists == 0b111 and list(packed.balance)[:3] == [10, 0, 3]
+    _compare(ctx, models.MODEL_BANK, b.hdr, b.events, packed)
+    del accts
+
+
+def test_budget(ctx):
+    rng = random.Random(5)
+    hs = [histgen.random_history(rng, "ticket", 40, 1) for _ in range(500)]
+    b = codec.encode(models.TICKET, hs)
+    for budget in (1, 7, 100):
+        st, nd, _ = _compare(ctx, models.MODEL_TICKET, b.hdr, b.events, max_nodes=budget)
+        assert (nd <= budget).all()
+
+
+def test_encode_errors(ctx):
+    hdr = np.zeros(5, dtype=codec.HDR_DTYPE)
+    ev = np.zeros(8, dtype=codec.EV_DTYPE)
+    hdr[0] = (0, 2, 1, 0xFF, 0, 0)            # wrong model
+    hdr[1] = (0, 2, 0, 2, 0, 0)               # pid >= n_pid
+    hdr[2] = (0, 200, 1, 2, 0, 0)             # too many events / beyond buffer
+    hdr[3] = (6, 2, 1, 2, 0, 0)               # ok shape; bad code below
+    hdr[4] = (4, 2, 1, 2, 0, 0)               # valid: Open a / Created
+    ev[4] = (0, 0, 0, 0, 0)
+    ev[5] = (0x80, 0, 0, 0, 0)
+    ev[6] = (0, 9, 0, 0, 0)                   # unknown Bank request
+    ev[7] = (0x80, 0, 0, 0, 0)
+    st, nd, _, tot = ctx.check_arrays(models.MODEL_BANK, hdr, ev)
+    assert list(st) == [3, 3, 3, 3, 1]
+    assert tot["encode_errors"] == 4
+
+
+def test_device_resident_full_size(ctx):
+    """BASELINE config 2 at full size (1M histories) through the device entry
+    point; size-independent properties (all linearisable by construction,
+    totals == sums) plus an exact oracle comparison on a sample."""
+    torch = pytest.importorskip("torch")
+    n = 1_000_000
+    hdr, ev, bug = gen.generate_config("bank_4x16", 0, n)
+    dev = torch.device("cuda:0")
+    d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
+    d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
+    d_st = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_nd = torch.empty(n, dtype=torch.int64, device=dev)
+    d_tot = torch.zeros(8, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    ctx.check_device(models.MODEL_BANK, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev),
+                     d_st.data_ptr(), d_nd.data_ptr(), None, d_tot.data_ptr(), stream=stream)
+    torch.cuda.synchronize()
+    st = d_st.cpu().numpy()
+    nd = d_nd.cpu().numpy().astype(np.uint64)
+    tot = d_tot.cpu().numpy()
+    assert (st == codec.STATUS_LIN).all()
+    assert int(tot[0]) == n and int(tot[1]) == n and int(tot[7]) == int(nd.sum())
+    assert (nd >= 16).all()
+    idx = np.arange(0, n, 50)
+    st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr[idx], ev, threads=8)
+    assert np.array_equal(st_o, st[idx]) and np.array_equal(nd_o, nd[idx])
