@@ -83,6 +83,7 @@ bool in_i32(int64_t v) { return v >= INT32_MIN && v <= INT32_MAX; }
 int fill_model0(qsmd_ctx* c, uint32_t model_id, const void* model0, SearchArgs& a) {
     a.m0_exists = 0;
     a.m0_just = 0;
+    a.m0_small = 1;
     for (auto& v : a.m0_val) v = 0;
     if (!model0) return QSMD_OK;
     if (model_id == QSMD_MODEL_BANK) {
@@ -101,6 +102,8 @@ int fill_model0(qsmd_ctx* c, uint32_t model_id, const void* model0, SearchArgs& 
         a.m0_just = m->is_just;
         a.m0_val[0] = m->is_just ? m->n : 0;
     }
+    for (int64_t v : a.m0_val)
+        if (v < -(1 << 18) || v >= (1 << 18)) a.m0_small = 0;   // stage 0 holds 19-bit values
     return QSMD_OK;
 }
 
@@ -210,7 +213,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.defer_list = l0;
     a0.defer_count = cnt + 0;
     a0.partials = part;
-    HIP_TRY(c, launch_stage(0, a0, (uint32_t)g0, s), "stage 0 launch");
+    HIP_TRY(c, launch_compact(a0, (uint32_t)g0, s), "stage 0 launch");
     HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
     // stage 1: histories with 33..64 events
     SearchArgs a1 = a;

@@ -30,6 +30,7 @@ struct SearchArgs {
     // initial model (model0): Bank exists + balances / Ticket just + n (val[0])
     uint32_t m0_exists;
     uint32_t m0_just;
+    uint32_t m0_small;            // every model0 value within 19-bit signed (stage 0)
     int64_t m0_val[QSMD_BANK_MAX_ACCOUNTS];
     // outputs
     uint8_t* status;
@@ -39,8 +40,9 @@ struct SearchArgs {
     uint32_t* timed_out;          // set to 1 if the time limit fired
 };
 
-// Stage kernels: each returns the number of blocks it launched (for the
-// partials buffer layout) through *blocks.
+// Stage 0 (csrc/compact.hip): <= 32 events, <= 8 pids, 19-bit values.
+hipError_t launch_compact(const SearchArgs& a, uint32_t grid, hipStream_t s);
+// Stages 1 and 2 (csrc/search.hip): list mode over the deferred histories.
 hipError_t launch_stage(int stage, const SearchArgs& a, uint32_t grid, hipStream_t s);
 uint32_t stage_lanes(int stage);
 uint32_t stage_max_events(int stage);

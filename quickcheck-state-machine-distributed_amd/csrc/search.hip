@@ -101,15 +101,24 @@ __global__ __launch_bounds__(LANES) void lane_search(SearchArgs a) {
         if (ok) {
             for (uint32_t p = 0; p < n_pid; ++p) s_pm[p][lane] = MaskT{};
             const uint2* evp = a.events + H.ev_off;
-            for (uint32_t e = 0; e < n_ev; ++e) {
-                const uint2 x = evp[e];
-                const Ev ev{x.x, (int32_t)x.y};
-                const uint32_t p = ev.pid();
-                ok = ok && p < n_pid && valid_event<MODEL>(ev);
-                s_ev[e][lane] = x;
-                const MaskT bit = Ops::bit((int)e);
-                if (ev.is_resp()) RESP |= bit; else INV |= bit;
-                if (p < n_pid) s_pm[p][lane] = s_pm[p][lane] | bit;
+            for (uint32_t e0 = 0; e0 < n_ev; e0 += 8) {
+                uint2 xs[8];                       // 8 independent loads in flight
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k)
+                    xs[k] = e0 + k < n_ev ? evp[e0 + k] : make_uint2(0u, 0u);
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k) {
+                    const uint32_t e = e0 + k;
+                    if (e >= n_ev) break;
+                    const uint2 x = xs[k];
+                    const Ev ev{x.x, (int32_t)x.y};
+                    const uint32_t p = ev.pid();
+                    ok = ok && p < n_pid && valid_event<MODEL>(ev);
+                    s_ev[e][lane] = x;
+                    const MaskT bit = Ops::bit((int)e);
+                    if (ev.is_resp()) RESP |= bit; else INV |= bit;
+                    if (p < n_pid) s_pm[p][lane] = s_pm[p][lane] | bit;
+                }
             }
         }
         if (!ok) {
