@@ -1,0 +1,175 @@
+"""CPU tests of the host side: the C ABI library loads and exports every
+symbol include/*.h declares (no compute calls), the marshaller, the
+generator, and the host mirrors of `trace` / `wellformed`
+(src/Linearisability.hs:73-135)."""
+
+import ctypes
+import os
+import random
+import re
+
+import numpy as np
+import pytest
+
+import histgen
+import linearise_lists as LL
+import oracle_c
+from kats import KAT2_TRACE, KATS
+from qsmd import codec, device, gen, models
+from qsmd.linearisability import NotSequential, replay_witness, trace, wellformed
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared(header):
+    txt = open(os.path.join(ROOT, "include", header)).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(qsmd_\w+)\s*\(", txt)))
+
+
+def test_abi_exports_every_declared_symbol():
+    lib = ctypes.CDLL(device.LIB_PATH)
+    names = _declared("qsmd.h")
+    assert "qsmd_check_batch" in names and "qsmd_check_batch_device" in names
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(device.EXPORTS) == set(names)
+    assert device.load_library().qsmd_abi_version() == 1
+
+
+def test_gen_abi_exports():
+    lib = ctypes.CDLL(gen.LIB_PATH)
+    for n in _declared("qsmd_gen.h"):
+        assert hasattr(lib, n), n
+
+
+def test_struct_layouts():
+    assert codec.HDR_DTYPE.itemsize == 16 and codec.EV_DTYPE.itemsize == 8
+    assert ctypes.sizeof(device.Totals) == 64
+    assert ctypes.sizeof(models.BankModel) == 72 and ctypes.sizeof(models.TicketModel) == 16
+    assert ctypes.sizeof(gen.GenParams) == 48
+
+
+def test_no_device_is_loud():
+    # No GPU in this container: opening a context must fail, never fall back.
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(device.DeviceError):
+        device.Context(0)
+
+
+def test_codec_round_trip():
+    rng = random.Random(2)
+    for model in ("ticket", "bank"):
+        sub = [histgen.random_history(rng, model, rng.randint(0, 20), rng.randint(1, 5))
+               for _ in range(200)]
+        b = codec.encode(models.BY_NAME[model], sub)
+        for i, h in enumerate(sub):
+            if i in b.encode_errors:
+                continue
+            assert codec.decode_history(b, i) == h
+
+
+def test_codec_pid_mapping_is_verdict_invariant():
+    # Eq pid only: renaming pids cannot change the verdict (src/Linearisability.hs:30-45)
+    model, hist, status, nodes = KATS["KAT3_distinct_pids"]
+    ren = [({"c1": "pid://x:9", "c2": "pid://y:3"}[p], e) for p, e in hist]
+    assert LL.check(model, ren)[:2] == (status, nodes)
+    b1 = codec.encode(models.TICKET, [hist])
+    b2 = codec.encode(models.TICKET, [ren])
+    assert np.array_equal(b1.events, b2.events)
+
+
+def test_codec_encode_errors():
+    bad = [
+        [("p", ("L", "Jump"))],                                      # unknown constructor
+        [("p", ("R", ("Number", 2**31)))],                           # outside int32
+        [("p", ("L", "Reset"))] * 129,                               # > 128 events
+    ]
+    b = codec.encode(models.TICKET, bad)
+    assert set(b.encode_errors) == {0, 1, 2}
+    assert (b.hdr["model_id"] == codec.BAD_MODEL).all()
+    accts = [(f"a{i}", ("L", ("OpenAccount", f"a{i}"))) for i in range(9)]
+    b = codec.encode(models.BANK, [accts])
+    assert 0 in b.encode_errors                                      # > 8 accounts
+    st, nd, _ = oracle_c.check_batch(models.MODEL_BANK, b.hdr, b.events)
+    assert st[0] == codec.STATUS_ENCODE_ERROR and nd[0] == 0
+
+
+def test_generator_deterministic_and_shardable():
+    p = gen.params(**gen.CONFIGS["bank_4x16"])
+    h1, e1, _ = gen.generate(p, 0, 3000, threads=4)
+    h2, e2, _ = gen.generate(p, 0, 3000, threads=1)
+    assert np.array_equal(e1, e2) and np.array_equal(h1, h2)
+    # rank r of N generates [r*n, (r+1)*n) of the same global stream
+    _, e3, _ = gen.generate(p, 1000, 2000, threads=2)
+    assert np.array_equal(e3, e1[1000 * 32:])
+
+
+@pytest.mark.parametrize("name", sorted(gen.CONFIGS))
+def test_generator_configs_are_wellformed_and_as_specified(name):
+    n = 400 if name != "ticket_8x64" else 50
+    hdr, ev, bug = gen.generate_config(name, 0, n)
+    cfg = gen.CONFIGS[name]
+    model = models.BY_ID[cfg["model_id"]]
+    assert (hdr["n_ev"] == 2 * cfg["n_ops"]).all()
+    b = codec.Batch(model, hdr, ev, [{i: i for i in range(8)}] * n, [{i: i for i in range(8)}] * n)
+    for i in range(0, n, 7):
+        hist = codec.decode_history(b, i)
+        pids = sorted({p for p, _ in hist})
+        # per-client pids are well-formed; the shared pid of the reference's
+        # parallel TicketDispenser property (Q1) is not (and is not checked there)
+        if cfg["pid_mode"] == gen.PID_PER_CLIENT:
+            assert wellformed(pids, hist) is None
+    st, nd, _ = oracle_c.check_batch(cfg["model_id"], hdr, ev, threads=4, max_nodes=10**6)
+    if cfg.get("p_bug", 0) == 0 and cfg.get("pid_mode", 0) == gen.PID_PER_CLIENT:
+        assert (st == codec.STATUS_LIN).all()           # linearisable by construction
+    if name == "ticket_2x10":
+        assert (st == codec.STATUS_NONLIN).any()        # Q1: shared pid + reordering fails
+    if name == "bank_4x16_bugs":
+        assert 0.3 < bug.mean() < 0.7
+        assert (st[bug == 0] == codec.STATUS_LIN).all()
+        assert (st[bug == 1] == codec.STATUS_NONLIN).any()
+
+
+def test_trace_matches_reference_example():
+    _, hist, _, _ = KATS["KAT2_reference_example"]
+    T = models.TICKET
+    assert trace(T.transition, T.init_model, hist) == KAT2_TRACE
+    pid = "pid://127.0.0.1:10501:0:8"
+    assert trace(T.transition, None, [(pid, e) for _, e in hist]) == KAT2_TRACE
+
+
+def test_wellformed_cases():
+    L, R = codec.Left, codec.Right
+    ok = [("a", L("Reset")), ("b", L("Reset")), ("a", R("Ok")), ("b", R("Ok"))]
+    assert wellformed(["a", "b"], ok) is None
+    assert wellformed(["a"], [("a", R("Ok"))]) == NotSequential("FirstEventIsntInvocation", ("a", "Ok"))
+    assert wellformed(["a"], [("a", L("Reset")), ("a", L("Reset"))]).kind == "InvocationFollowedByInvocation"
+    assert wellformed(["a"], [("a", L("Reset")), ("a", R("Ok")), ("a", R("Ok"))]).kind == "LoneResponse"
+    assert wellformed(["a"], [("a", L("Reset")), ("a", R("Ok")), ("a", R("Ok")), ("a", R("Ok"))]).kind == \
+        "ResponseFollowedByResponse"
+    assert wellformed(["a"], [("a", L("Reset")), ("a", R("Ok")), ("a", R("Ok")), ("a", L("Reset"))]).kind == \
+        "ResponseFollowedByInvocation"
+    assert wellformed(["a"], [("a", L("Reset"))]) is None              # pending invocation
+
+
+def test_replay_witness_accepts_oracle_witnesses_and_rejects_others():
+    rng = random.Random(8)
+    checked = 0
+    for _ in range(3000):
+        model = rng.choice(["ticket", "bank"])
+        hist = histgen.wellformed_history(rng, model, rng.randint(1, 5), rng.randint(1, 3))
+        m = models.BY_NAME[model]
+        b = codec.encode(m, [hist])
+        st, nd, w = oracle_c.check_batch(m.model_id, b.hdr, b.events, witness=True)
+        if st[0] != codec.STATUS_LIN:
+            continue
+        wit = [int(x) for x in w[: len(hist)]]
+        wit = wit[: wit.index(0xFF)] if 0xFF in wit else wit
+        assert replay_witness(m, hist, wit)
+        if len(wit) >= 1:
+            assert not replay_witness(m, hist, wit[:-1]) or len(wit) == 0
+        checked += 1
+    assert checked > 50
