@@ -4,15 +4,26 @@
 // src/QuickCheckHelpers.hs:74) and of the 4x16 Bank benchmark.
 //
 // Same search as csrc/search.hip (src/Linearisability.hs:25-69 over the
-// Lemma L1 event bitset), re-laid out for latency: the only per-node LDS
-// traffic is ONE round trip that fetches the candidate invocation and its
-// response together (both addresses are computed in registers first: the pid
-// of every event is kept as 4-bit nibbles in 4 VGPRs and the per-pid event
-// masks in 8 VGPRs), and the model (Bank balances as i32, Ticket Maybe Int)
-// lives entirely in registers, indexed by unrolled select trees.  LDS holds
-// only the history (one u32 per event, [event][lane]) and one u32 per DFS
-// level ([level][lane]): 12 KiB per wavefront.  Histories outside these
-// bounds are deferred to stage 1 (search.hip) with a wave-aggregated append.
+// Lemma L1 event bitset), laid out for a divergent 64-lane wavefront where
+// each lane runs its own DFS:
+//   * per node, addresses come from registers (pids bit-sliced into three
+//     masks P0/P1/P2), so a node costs one LDS round trip for the candidate
+//     invocation + its response and (Bank) one for the two balances;
+//   * the DFS stack lives in registers: 8 bits per level (candidate index +
+//     the two pre-op "account exists" bits Bank's undo needs), 16 levels in
+//     4 VGPRs.  The TicketDispenser model needs no undo record at all: it is
+//     a function of (depth, mask of levels that applied Reset) -- after the
+//     last Reset the model is Just (#TakeTickets since), before any Reset it
+//     is model0 advanced by `succ <$>` once per level;
+//   * the model's post/next are table lookups and predicated arithmetic, not
+//     branches; Bank balances (i32) are the only model state in LDS;
+//   * LDS per wavefront: the history (one u32 per event) + Bank balances,
+//     [slot][lane] (bank = lane: conflict-free for any per-lane index),
+//     8-10 KiB;
+//   * staging issues 16 loads back to back per chunk (indices clamped into
+//     the history, no exec-masked branches).
+// Histories outside these bounds go to stage 1 (search.hip) through a
+// wave-aggregated append to the deferred list.
 #include <hip/hip_runtime.h>
 
 #include "internal.h"
@@ -23,8 +34,8 @@ namespace qsmd {
 namespace {
 
 constexpr int C_MAXEV = 32;
-constexpr int C_MAXD = C_MAXEV / 2;
 constexpr int C_LANES = 64;
+constexpr int C_CHUNK = 16;
 constexpr int32_t V19_MIN = -(1 << 18), V19_MAX = (1 << 18) - 1;
 
 // compressed event: pid 3 | resp 1 | code 3 | a 3 | b 3 | val 19 (signed)
@@ -33,36 +44,41 @@ __device__ __forceinline__ uint32_t c_a(uint32_t w) { return (w >> 7) & 7u; }
 __device__ __forceinline__ uint32_t c_b(uint32_t w) { return (w >> 10) & 7u; }
 __device__ __forceinline__ int32_t c_val(uint32_t w) { return (int32_t)w >> 13; }
 
-// v[i] for a per-lane i, as a VGPR select tree.  The empty asm makes each
-// element an opaque register value: without it hipcc folds the select tree
-// back into a dynamically indexed private array (scratch memory).
-template <typename T>
-__device__ __forceinline__ T sel8(const T (&v)[8], uint32_t i) {
-    T x[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        x[q] = v[q];
-        asm volatile("" : "+v"(x[q]));
-    }
-    const T a0 = (i & 1u) ? x[1] : x[0], a1 = (i & 1u) ? x[3] : x[2];
-    const T a2 = (i & 1u) ? x[5] : x[4], a3 = (i & 1u) ? x[7] : x[6];
-    const T b0 = (i & 2u) ? a1 : a0, b1 = (i & 2u) ? a3 : a2;
-    return (i & 4u) ? b1 : b0;
-}
+__device__ __forceinline__ uint32_t below32(uint32_t r) { return (uint32_t)((1ull << r) - 1ull); }
 
-template <typename T>
-__device__ __forceinline__ void put8(T (&v)[8], uint32_t i, T x) {
-#pragma unroll
-    for (uint32_t q = 0; q < 8; ++q) v[q] = (q == i) ? x : v[q];
-}
-
-__device__ __forceinline__ uint32_t below32(uint32_t r) { return r >= 32u ? ~0u : (1u << r) - 1u; }
-
+// candidates: remaining invocations before the first remaining response
+// (takeInvocations, src/Linearisability.hs:25-28); branch-free
 __device__ __forceinline__ uint32_t cands(uint32_t rem, uint32_t INV, uint32_t RESP) {
-    const uint32_t rr = rem & RESP;
-    const uint32_t R = rr ? (uint32_t)__builtin_ctz(rr) : 32u;
+    const uint32_t R = (uint32_t)__builtin_ctzll((uint64_t)(rem & RESP) | (1ull << 32));
     return rem & INV & below32(R);
 }
+
+// Expected Bank response constructor of `post` (test/Bank.hs:118-131) as a
+// table lookup, index = code*4 + ex_a*2 + ge (3 bits per entry):
+//   Open: ex_a ? AccountAlreadyExists : AccountCreated   Deposit: DepositMade
+//   Withdraw: ge ? WithdrawalMade : InsufficientFunds    CheckBalance: Balance
+//   Transfer: ge ? TransferMade : InsufficientFunds
+constexpr uint64_t bank_exp_table() {
+    uint64_t t = 0;
+    for (uint32_t code = 0; code < 5; ++code)
+        for (uint32_t exa = 0; exa < 2; ++exa)
+            for (uint32_t ge = 0; ge < 2; ++ge) {
+                uint32_t e = QSMD_BANK_INSUFFICIENT_FUNDS;
+                if (code == QSMD_BANK_OPEN_ACCOUNT) e = exa ? QSMD_BANK_ACCOUNT_ALREADY_EXISTS : QSMD_BANK_ACCOUNT_CREATED;
+                else if (code == QSMD_BANK_DEPOSIT) e = QSMD_BANK_DEPOSIT_MADE;
+                else if (code == QSMD_BANK_WITHDRAW) e = ge ? QSMD_BANK_WITHDRAWAL_MADE : QSMD_BANK_INSUFFICIENT_FUNDS;
+                else if (code == QSMD_BANK_CHECK_BALANCE) e = QSMD_BANK_BALANCE;
+                else e = ge ? QSMD_BANK_TRANSFER_MADE : QSMD_BANK_INSUFFICIENT_FUNDS;
+                t |= (uint64_t)e << (3 * (code * 4 + exa * 2 + ge));
+            }
+    return t;
+}
+constexpr uint64_t kBankExp = bank_exp_table();
+// per request code: sign of the step on account a (Deposit +1, Withdraw and
+// Transfer -1, Open / CheckBalance 0); an absent account is created with the
+// money exactly when the sign is non-zero (insertWith, test/Bank.hs:96-97)
+constexpr uint32_t kBankNeg = (1u << QSMD_BANK_WITHDRAW) | (1u << QSMD_BANK_TRANSFER);
+constexpr uint32_t kBankPos = (1u << QSMD_BANK_DEPOSIT);
 
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -74,19 +90,56 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
+// include/qsmd.h encoding rules, branch-free.
+template <uint32_t MODEL>
+__device__ __forceinline__ bool valid_bits(uint32_t lo) {
+    const uint32_t c = (lo >> 8) & 0xFFu, ea = (lo >> 16) & 0xFFu, eb = lo >> 24;
+    if constexpr (MODEL == QSMD_MODEL_TICKET) {
+        return c <= 1u;
+    } else {
+        const bool resp = (lo & 0x80u) != 0u;
+        const bool inv_ok = (c <= QSMD_BANK_TRANSFER) & (ea < 8u) & ((c != QSMD_BANK_TRANSFER) | (eb < 8u));
+        return resp ? (c <= QSMD_BANK_BALANCE) : inv_ok;
+    }
+}
+
+// The DFS stack: 16 levels x 8 bits in 4 VGPRs.  Selection goes through an
+// empty asm so hipcc keeps it a register select (it otherwise turns the
+// select tree into a scratch-memory indexed load).
+struct Stack16 {
+    uint32_t w[4];
+    __device__ __forceinline__ uint32_t word(uint32_t d) const {
+        uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3];
+        asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+        const uint32_t k = d >> 2;
+        const uint32_t lo = (k & 1u) ? x1 : x0, hi = (k & 1u) ? x3 : x2;
+        return (k & 2u) ? hi : lo;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t d) const {
+        return (word(d) >> ((d & 3u) * 8u)) & 0xFFu;
+    }
+    __device__ __forceinline__ void put(uint32_t d, uint32_t v) {
+        const uint32_t k = d >> 2, sh = (d & 3u) * 8u;
+        const uint32_t keep = ~(0xFFu << sh), ins = v << sh;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) w[q] = (q == k) ? ((w[q] & keep) | ins) : w[q];
+    }
+};
+
 }  // namespace
 
 template <uint32_t MODEL>
 __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
     constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
     __shared__ uint32_t s_ev[C_MAXEV][C_LANES];
-    __shared__ uint32_t s_st[C_MAXD][C_LANES];
+    __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
 
     const int lane = threadIdx.x;
     const uint64_t total = a.n_hist;
     uint32_t c_lin = 0, c_nonlin = 0, c_err = 0, c_enc = 0, c_budget = 0;
     uint64_t c_nodes = 0;
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t node_limit = a.max_nodes ? a.max_nodes : ~0ull;
 
     for (uint64_t base = (uint64_t)blockIdx.x * C_LANES; base < total;
          base += (uint64_t)gridDim.x * C_LANES) {
@@ -101,35 +154,35 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
                             n_pid <= QSMD_MAX_PIDS && (uint64_t)H.ev_off + n_ev <= a.n_events;
         const bool small = enc_ok && n_ev <= (uint32_t)C_MAXEV && n_pid <= 8u && a.m0_small;
 
-        // ---- stage the history: 16 independent 8-byte loads in flight per
-        //      chunk, then (branch-free) compress into LDS and build the
-        //      register masks.  Pids are kept bit-sliced: P0/P1/P2 hold bit
-        //      0/1/2 of every event's pid, so "events with the pid of event
-        //      j" is a handful of VALU ops (same_pid below), no table.
+        // ---- stage: C_CHUNK loads in flight (index clamped into the
+        //      history), then compress into LDS and build the register masks.
+        //      Pids are bit-sliced: P0/P1/P2 hold bit 0/1/2 of each event's pid.
         uint32_t INV = 0, RESP = 0, P0 = 0, P1 = 0, P2 = 0;
         bool ok = enc_ok, fits = small;
-        if (small) {
+        if (small && n_ev > 0) {
             const uint2* evp = a.events + H.ev_off;
+            const uint32_t last = n_ev - 1u;
 #pragma unroll
-            for (int c = 0; c < C_MAXEV / 16; ++c) {
-                uint2 x[16];
+            for (uint32_t c0 = 0; c0 < (uint32_t)C_MAXEV; c0 += C_CHUNK) {
+                uint2 x[C_CHUNK];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const uint32_t e = (uint32_t)(c * 16 + k);
-                    x[k] = e < n_ev ? evp[e] : make_uint2(0u, 0u);
+                for (uint32_t k = 0; k < (uint32_t)C_CHUNK; ++k) {
+                    const uint32_t e = c0 + k;
+                    x[k] = evp[e < last ? e : last];
                 }
 #pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const uint32_t e = (uint32_t)(c * 16 + k);
+                for (uint32_t k = 0; k < (uint32_t)C_CHUNK; ++k) {
+                    const uint32_t e = c0 + k;
+                    const uint32_t lo = x[k].x;
+                    const int32_t val = (int32_t)x[k].y;
                     const bool in = e < n_ev;
-                    const Ev ev{x[k].x, (int32_t)x[k].y};
-                    const uint32_t p = ev.pid();
-                    ok = ok & (!in | ((p < n_pid) & valid_event<MODEL>(ev)));
-                    fits = fits & (!in | ((ev.val >= V19_MIN) & (ev.val <= V19_MAX)));
-                    const uint32_t resp = ev.is_resp() ? 1u : 0u;
-                    s_ev[e][lane] = (p & 7u) | (resp << 3) | ((ev.code() & 7u) << 4) |
-                                    ((ev.a() & 7u) << 7) | ((ev.b() & 7u) << 10) |
-                                    ((uint32_t)ev.val << 13);
+                    const uint32_t p = lo & 0x7Fu;
+                    ok = ok & (!in | ((p < n_pid) & valid_bits<MODEL>(lo)));
+                    fits = fits & (!in | ((val >= V19_MIN) & (val <= V19_MAX)));
+                    const uint32_t resp = (lo >> 7) & 1u;
+                    s_ev[e][lane] = (p & 7u) | (resp << 3) | (((lo >> 8) & 7u) << 4) |
+                                    (((lo >> 16) & 7u) << 7) | (((lo >> 24) & 7u) << 10) |
+                                    ((uint32_t)val << 13);
                     const uint32_t bit = in ? (1u << e) : 0u;
                     RESP |= resp ? bit : 0u;
                     INV |= resp ? 0u : bit;
@@ -162,23 +215,29 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
         int status = -1;
         uint64_t nodes = 0;
         uint32_t depth = 0;
+        Stack16 stk{{0u, 0u, 0u, 0u}};
         if (!ok) {
             status = QSMD_STATUS_ENCODE_ERROR;
         } else if (n_ev == 0) {
             status = QSMD_STATUS_LINEARISABLE;                       // :59
         } else {
-            // ---- model in registers
-            uint32_t ex = a.m0_exists, neg = 0;
-            int32_t bal[8];
-            uint32_t just = a.m0_just;
-            int32_t tn = (int32_t)a.m0_val[0];
+            // ---- model state.  Bank: exists / negative-balance masks in
+            //      registers, balances in LDS.  Ticket: RS = levels that applied
+            //      Reset; the model at depth d is derived from (d, RS).
+            uint32_t ex = a.m0_exists, neg = 0, RS = 0;
+            if constexpr (BANK) {
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                bal[q] = ((ex >> q) & 1u) ? (int32_t)a.m0_val[q] : 0;
-                neg |= (((ex >> q) & 1u) && bal[q] < 0) ? (1u << q) : 0u;
+                for (int q = 0; q < QSMD_BANK_MAX_ACCOUNTS; ++q) {
+                    const bool e = (ex >> q) & 1u;
+                    const int32_t v = e ? (int32_t)a.m0_val[q] : 0;
+                    s_bal[q][lane] = v;
+                    neg |= (e && v < 0) ? (1u << q) : 0u;
+                }
             }
+            const uint32_t m0_just = a.m0_just;
+            const int32_t m0_n = (int32_t)a.m0_val[0];
 
-            uint32_t rem = INV | RESP;
+            uint32_t rem = ALL;
             uint32_t cand = cands(rem, INV, RESP);
             bool found = false;
             uint32_t iter = 0;
@@ -189,38 +248,35 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
                         break;
                     }
                     if (depth == 0) { status = QSMD_STATUS_NONLINEARISABLE; break; }
-                    // ---- backtrack
+                    // ---- backtrack: restore the parent level exactly
                     --depth;
-                    const uint32_t st = s_st[depth][lane];
+                    const uint32_t st = stk.get(depth);
                     const uint32_t j = st & 31u;
-                    const uint32_t cj = s_ev[j][lane];
-                    const uint32_t pmj = same_pid(j);
-                    const uint32_t gone = ~rem & pmj;
+                    const uint32_t gone = ~rem & same_pid(j);
                     rem |= (1u << (31 - __builtin_clz(gone & INV))) |
                            (1u << (31 - __builtin_clz(gone & RESP)));
                     if constexpr (BANK) {
-                        const uint32_t code = c_code(cj);
-                        if (code != QSMD_BANK_CHECK_BALANCE) {
-                            const uint32_t ia = c_a(cj), ib = c_b(cj);
-                            const int32_t m = c_val(cj);
-                            const uint32_t pa = (st >> 5) & 1u, pb = (st >> 6) & 1u;
-                            if (code == QSMD_BANK_TRANSFER) {
-                                const bool mid = pb || ia == ib;
-                                put8(bal, ib, mid ? sel8(bal, ib) - m : 0);
-                            }
-                            const int32_t delta = code == QSMD_BANK_DEPOSIT ? m
-                                                : code == QSMD_BANK_OPEN_ACCOUNT ? 0 : -m;
-                            put8(bal, ia, pa ? sel8(bal, ia) - delta : 0);
-                            ex = (ex & ~(1u << ia)) | (pa << ia);
-                            if (code == QSMD_BANK_TRANSFER) ex = (ex & ~(1u << ib)) | (pb << ib);
-                            const int32_t va = sel8(bal, ia), vb = sel8(bal, ib);
-                            neg = (neg & ~((1u << ia) | (1u << ib))) |
-                                  ((((ex >> ia) & 1u) && va < 0) ? (1u << ia) : 0u) |
-                                  ((((ex >> ib) & 1u) && vb < 0) ? (1u << ib) : 0u);
-                        }
+                        const uint32_t cj = s_ev[j][lane];
+                        const uint32_t code = c_code(cj), ia = c_a(cj), ib = c_b(cj);
+                        const int32_t m = c_val(cj);
+                        const uint32_t pa = (st >> 5) & 1u, pb = (st >> 6) & 1u;
+                        const uint32_t tr = code == QSMD_BANK_TRANSFER ? 1u : 0u;
+                        const int32_t ba = s_bal[ia][lane], bb = s_bal[ib][lane];
+                        // undo Transfer's deposit on b, then the step on a
+                        const int32_t rb = (pb | (ia == ib)) ? bb - m : 0;
+                        const int32_t cur_a = (tr & (ia == ib)) ? rb : ba;
+                        const int32_t sa = (int32_t)((kBankPos >> code) & 1u) - (int32_t)((kBankNeg >> code) & 1u);
+                        const int32_t ra = pa ? cur_a - sa * m : 0;
+                        const int32_t fb = tr ? rb : bb;
+                        s_bal[ib][lane] = fb;                  // a no-op unless Transfer
+                        s_bal[ia][lane] = ra;                  // written last (ia == ib)
+                        ex = (ex & ~((1u << ia) | (tr << ib))) | (pa << ia) | ((tr & pb) << ib);
+                        const int32_t vb = ia == ib ? ra : fb;
+                        neg &= ~((1u << ia) | (1u << ib));
+                        neg |= ((ra < 0) ? ((ex >> ia) & 1u) : 0u) << ia;
+                        neg |= ((vb < 0) ? ((ex >> ib) & 1u) : 0u) << ib;
                     } else {
-                        just = (st >> 5) & 1u;
-                        tn = (int32_t)st >> 6;
+                        RS &= ~(1u << depth);
                     }
                     cand = cands(rem, INV, RESP) & ~below32(j + 1u);
                     found = true;
@@ -232,64 +288,65 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
                     status = QSMD_STATUS_BUDGET;
                     break;
                 }
-                // ---- next candidate: addresses from registers, one LDS round trip
+                // ---- try the next candidate
                 const uint32_t j = (uint32_t)__builtin_ctz(cand);
                 cand &= cand - 1u;
                 const uint32_t pmj = same_pid(j);
                 const uint32_t rr = rem & pmj & RESP;
                 if (!rr) continue;                    // findResponse => []: no child
                 found = true;
-                if (a.max_nodes && nodes >= a.max_nodes) { status = QSMD_STATUS_BUDGET; break; }
+                if (nodes >= node_limit) { status = QSMD_STATUS_BUDGET; break; }
                 ++nodes;
                 const uint32_t r = (uint32_t)__builtin_ctz(rr);
-                const uint32_t cj = s_ev[j][lane];
-                const uint32_t cr = s_ev[r][lane];
+                const uint32_t cj = s_ev[j][lane], cr = s_ev[r][lane];
                 const uint32_t code = c_code(cj), rc = c_code(cr);
                 const int32_t m = c_val(cj), rv = c_val(cr);
                 uint32_t stw;
                 if constexpr (BANK) {
-                    // post (test/Bank.hs:118-131)
                     const uint32_t ia = c_a(cj), ib = c_b(cj);
-                    const bool ex_a = (ex >> ia) & 1u;
-                    const int32_t bal_a = sel8(bal, ia);
-                    if (neg) continue;                            // invariant model
-                    const uint32_t exp = bank_expected(code, ex_a, bal_a, m);
-                    if (rc != exp) continue;
-                    if (code == QSMD_BANK_CHECK_BALANCE) {
-                        if (!ex_a) { status = QSMD_STATUS_MODEL_ERROR; break; }   // Map.!
-                        if (rv != bal_a) continue;
+                    const int32_t bal_a = s_bal[ia][lane], bal_b = s_bal[ib][lane];
+                    const uint32_t ex_a = (ex >> ia) & 1u, ex_b = (ex >> ib) & 1u;
+                    // post (test/Bank.hs:118-131): invariant && expected response
+                    const uint32_t tr = code == QSMD_BANK_TRANSFER ? 1u : 0u;
+                    const bool chk = code == QSMD_BANK_CHECK_BALANCE;
+                    const uint32_t ge = (ex_a & (bal_a >= m ? 1u : 0u));   // lookup >= Just m
+                    const uint32_t exp = (uint32_t)(kBankExp >> (3u * (code * 4u + ex_a * 2u + ge))) & 7u;
+                    const bool inv_ok = neg == 0u;
+                    if (inv_ok & chk & (rc == QSMD_BANK_BALANCE) & !ex_a) {   // Map.! raises
+                        status = QSMD_STATUS_MODEL_ERROR;
+                        break;
                     }
-                    // descend: next' (test/Bank.hs:92-101)
-                    const uint32_t pb = (ex >> ib) & 1u;
-                    stw = j | ((ex_a ? 1u : 0u) << 5) | (pb << 6);
-                    if (code != QSMD_BANK_CHECK_BALANCE) {
-                        int32_t na;
-                        if (code == QSMD_BANK_OPEN_ACCOUNT) na = ex_a ? bal_a : 0;
-                        else if (code == QSMD_BANK_DEPOSIT) na = ex_a ? bal_a + m : m;
-                        else na = ex_a ? bal_a - m : m;       // Withdraw / Transfer's withdraw
-                        put8(bal, ia, na);
-                        ex |= 1u << ia;
-                        if (code == QSMD_BANK_TRANSFER) {
-                            const bool ex_b = (ex >> ib) & 1u;
-                            put8(bal, ib, ex_b ? sel8(bal, ib) + m : m);
-                            ex |= 1u << ib;
-                        }
-                        const int32_t va = sel8(bal, ia), vb = sel8(bal, ib);
-                        neg = (neg & ~((1u << ia) | (1u << ib))) |
-                              ((((ex >> ia) & 1u) && va < 0) ? (1u << ia) : 0u) |
-                              ((((ex >> ib) & 1u) && vb < 0) ? (1u << ib) : 0u);
-                    }
+                    if (!(inv_ok & (rc == exp) & (!chk | (rv == bal_a)))) continue;
+                    // next' (test/Bank.hs:92-101) on a, then Transfer's deposit on b
+                    stw = j | (ex_a << 5) | (ex_b << 6);
+                    const int32_t sa = (int32_t)((kBankPos >> code) & 1u) - (int32_t)((kBankNeg >> code) & 1u);
+                    const int32_t na = ex_a ? bal_a + sa * m : (sa != 0 ? m : 0);
+                    ex |= (chk ? 0u : 1u) << ia;
+                    const int32_t bo = ia == ib ? na : bal_b;
+                    const int32_t nb = ((ex >> ib) & 1u) ? bo + m : m;
+                    const int32_t fb = tr ? nb : bo;
+                    s_bal[ia][lane] = na;
+                    s_bal[ib][lane] = fb;                     // a no-op unless Transfer
+                    ex |= tr << ib;
+                    const int32_t va = ia == ib ? fb : na;
+                    neg &= ~((1u << ia) | (1u << ib));
+                    neg |= ((va < 0) ? ((ex >> ia) & 1u) : 0u) << ia;
+                    neg |= ((fb < 0) ? ((ex >> ib) & 1u) : 0u) << ib;
                 } else {
+                    // model at this depth: Just (#TT since the last Reset), or
+                    // model0 advanced by succ <$> once per level
+                    const uint32_t just = RS ? 1u : m0_just;
+                    const int32_t tn = RS ? (int32_t)(depth - 1u - (31u - __builtin_clz(RS | 1u)))
+                                          : m0_n + (m0_just ? (int32_t)depth : 0);
                     // postcondition (test/TicketDispenser.hs:99-102)
-                    const bool tt = code == QSMD_TICKET_TAKE_TICKET && rc == QSMD_TICKET_NUMBER &&
-                                    just && rv == tn + 1;
-                    const bool rs = code == QSMD_TICKET_RESET && rc == QSMD_TICKET_OK;
-                    if (!(tt || rs)) continue;
-                    stw = j | (just << 5) | ((uint32_t)tn << 6);
-                    if (code == QSMD_TICKET_TAKE_TICKET) tn += (int32_t)just;   // succ <$> m
-                    else { just = 1u; tn = 0; }                                 // Just 0
+                    const bool tt = code == QSMD_TICKET_TAKE_TICKET;
+                    const bool okp = tt ? (rc == QSMD_TICKET_NUMBER) & (just != 0u) & (rv == tn + 1)
+                                        : rc == QSMD_TICKET_OK;
+                    if (!okp) continue;
+                    stw = j;
+                    RS |= (tt ? 0u : 1u) << depth;     // transition: Reset => Just 0
                 }
-                s_st[depth][lane] = stw;
+                stk.put(depth, stw);
                 ++depth;
                 const uint32_t fi = rem & pmj & INV;
                 rem &= ~((fi & (0u - fi)) | (1u << r));
@@ -302,7 +359,7 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
         if (a.nodes) a.nodes[h] = nodes;
         if (a.witness && status == QSMD_STATUS_LINEARISABLE) {
             uint8_t* w = a.witness + H.ev_off;
-            for (uint32_t d = 0; d < depth; ++d) w[d] = (uint8_t)(s_st[d][lane] & 31u);
+            for (uint32_t d = 0; d < depth; ++d) w[d] = (uint8_t)(stk.get(d) & 31u);
             if (depth < n_ev) w[depth] = QSMD_WITNESS_END;
         }
         c_lin += status == QSMD_STATUS_LINEARISABLE;
