@@ -189,6 +189,11 @@ int qsmd_check_batch_device(qsmd_ctx* ctx, uint32_t model_id,
  * 120000 ms; 0 disables).  Not part of the reference semantics. */
 int qsmd_set_time_limit_ms(qsmd_ctx* ctx, uint64_t ms);
 
+/* Tuning knob: cap on the number of workgroups of the first search stage
+ * (beyond it each workgroup loops over several groups of 64 histories).
+ * Default 65536.  Does not change any result. */
+int qsmd_set_stage0_grid(qsmd_ctx* ctx, uint64_t max_blocks);
+
 /* Device time (ms, HIP events on the launch stream) of the search kernels of
  * the most recent check call, measured once that stream has completed. */
 int qsmd_last_kernel_ms(qsmd_ctx* ctx, float* ms_out);

@@ -36,13 +36,13 @@ struct qsmd_ctx {
     uint64_t n_calls = 0;                // calls recorded since the last reset
     bool timed = false;
     uint64_t time_limit_ms = 120000;   // safety net per search launch
+    uint64_t stage0_max_grid = 65536;  // tuning: cap on stage-0 workgroups (grid-stride beyond)
 };
 
 namespace {
 
 constexpr uint32_t kStage1Grid = 1024;   // list-mode stages: grid-stride
 constexpr uint32_t kStage2Grid = 1024;
-constexpr uint64_t kStage0MaxGrid = 65536;
 constexpr uint64_t kTimingSlots = 1024;
 
 int fail(qsmd_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
@@ -150,6 +150,12 @@ void qsmd_close(qsmd_ctx* c) {
     delete c;
 }
 
+int qsmd_set_stage0_grid(qsmd_ctx* c, uint64_t max_blocks) {
+    if (!c || max_blocks == 0 || max_blocks > 0x7FFFFFFFull) return QSMD_ERR_ARG;
+    c->stage0_max_grid = max_blocks;
+    return QSMD_OK;
+}
+
 int qsmd_set_time_limit_ms(qsmd_ctx* c, uint64_t ms) {
     if (!c) return QSMD_ERR_ARG;
     c->time_limit_ms = ms;
@@ -172,7 +178,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
 
     // ---- workspace: defer lists, counters, partials, internal totals
-    const uint64_t g0 = std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), kStage0MaxGrid);
+    const uint64_t g0 = std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), c->stage0_max_grid);
     const uint64_t n_part = g0 + kStage1Grid + kStage2Grid;
     const size_t off_cnt = 0;                                          // 4 x u32
     const size_t off_tot = 256;                                        // qsmd_totals

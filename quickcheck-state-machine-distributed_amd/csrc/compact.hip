@@ -243,11 +243,11 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
             uint32_t iter = 0;
             for (;;) {
                 if (!cand) {
-                    if (!found) {        // no children: leaf => True, root => False
-                        status = depth == 0 ? QSMD_STATUS_NONLINEARISABLE : QSMD_STATUS_LINEARISABLE;
+                    if (!found || depth == 0) {   // no children: leaf => True, root => False
+                        status = (!found && depth > 0) ? QSMD_STATUS_LINEARISABLE
+                                                       : QSMD_STATUS_NONLINEARISABLE;
                         break;
                     }
-                    if (depth == 0) { status = QSMD_STATUS_NONLINEARISABLE; break; }
                     // ---- backtrack: restore the parent level exactly
                     --depth;
                     const uint32_t st = stk.get(depth);
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
                     }
                     cand = cands(rem, INV, RESP) & ~below32(j + 1u);
                     found = true;
-                    continue;
+                    if (!cand) continue;
                 }
                 if (a.time_limit && ((++iter & 1023u) == 0u) &&
                     __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
@@ -288,19 +288,17 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
                     status = QSMD_STATUS_BUDGET;
                     break;
                 }
-                // ---- try the next candidate
+                // ---- try the next candidate: straight-line, predicated
                 const uint32_t j = (uint32_t)__builtin_ctz(cand);
                 cand &= cand - 1u;
                 const uint32_t pmj = same_pid(j);
                 const uint32_t rr = rem & pmj & RESP;
-                if (!rr) continue;                    // findResponse => []: no child
-                found = true;
-                if (nodes >= node_limit) { status = QSMD_STATUS_BUDGET; break; }
-                ++nodes;
-                const uint32_t r = (uint32_t)__builtin_ctz(rr);
+                const bool has = rr != 0u;             // findResponse => [] : no child
+                const uint32_t r = (uint32_t)__builtin_ctz(rr | 0x80000000u);
                 const uint32_t cj = s_ev[j][lane], cr = s_ev[r][lane];
                 const uint32_t code = c_code(cj), rc = c_code(cr);
                 const int32_t m = c_val(cj), rv = c_val(cr);
+                bool ok, err;
                 uint32_t stw;
                 if constexpr (BANK) {
                     const uint32_t ia = c_a(cj), ib = c_b(cj);
@@ -312,26 +310,26 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
                     const uint32_t ge = (ex_a & (bal_a >= m ? 1u : 0u));   // lookup >= Just m
                     const uint32_t exp = (uint32_t)(kBankExp >> (3u * (code * 4u + ex_a * 2u + ge))) & 7u;
                     const bool inv_ok = neg == 0u;
-                    if (inv_ok & chk & (rc == QSMD_BANK_BALANCE) & !ex_a) {   // Map.! raises
-                        status = QSMD_STATUS_MODEL_ERROR;
-                        break;
-                    }
-                    if (!(inv_ok & (rc == exp) & (!chk | (rv == bal_a)))) continue;
-                    // next' (test/Bank.hs:92-101) on a, then Transfer's deposit on b
+                    err = has & inv_ok & chk & (rc == QSMD_BANK_BALANCE) & !ex_a;   // Map.! raises
+                    ok = has & inv_ok & (rc == exp) & (!chk | (rv == bal_a));
+                    // next' (test/Bank.hs:92-101) on a, then Transfer's deposit on b;
+                    // stored unconditionally (the old values when !ok)
                     stw = j | (ex_a << 5) | (ex_b << 6);
                     const int32_t sa = (int32_t)((kBankPos >> code) & 1u) - (int32_t)((kBankNeg >> code) & 1u);
                     const int32_t na = ex_a ? bal_a + sa * m : (sa != 0 ? m : 0);
-                    ex |= (chk ? 0u : 1u) << ia;
+                    const uint32_t ex1 = ex | ((chk ? 0u : 1u) << ia);
                     const int32_t bo = ia == ib ? na : bal_b;
-                    const int32_t nb = ((ex >> ib) & 1u) ? bo + m : m;
+                    const int32_t nb = ((ex1 >> ib) & 1u) ? bo + m : m;
                     const int32_t fb = tr ? nb : bo;
-                    s_bal[ia][lane] = na;
-                    s_bal[ib][lane] = fb;                     // a no-op unless Transfer
-                    ex |= tr << ib;
+                    s_bal[ia][lane] = ok ? na : bal_a;
+                    s_bal[ib][lane] = ok ? fb : bal_b;
+                    const uint32_t ex2 = ex1 | (tr << ib);
                     const int32_t va = ia == ib ? fb : na;
-                    neg &= ~((1u << ia) | (1u << ib));
-                    neg |= ((va < 0) ? ((ex >> ia) & 1u) : 0u) << ia;
-                    neg |= ((fb < 0) ? ((ex >> ib) & 1u) : 0u) << ib;
+                    uint32_t neg2 = neg & ~((1u << ia) | (1u << ib));
+                    neg2 |= ((va < 0) ? ((ex2 >> ia) & 1u) : 0u) << ia;
+                    neg2 |= ((fb < 0) ? ((ex2 >> ib) & 1u) : 0u) << ib;
+                    ex = ok ? ex2 : ex;
+                    neg = ok ? neg2 : neg;
                 } else {
                     // model at this depth: Just (#TT since the last Reset), or
                     // model0 advanced by succ <$> once per level
@@ -340,18 +338,29 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
                                           : m0_n + (m0_just ? (int32_t)depth : 0);
                     // postcondition (test/TicketDispenser.hs:99-102)
                     const bool tt = code == QSMD_TICKET_TAKE_TICKET;
-                    const bool okp = tt ? (rc == QSMD_TICKET_NUMBER) & (just != 0u) & (rv == tn + 1)
-                                        : rc == QSMD_TICKET_OK;
-                    if (!okp) continue;
+                    err = false;
+                    ok = has & (tt ? (rc == QSMD_TICKET_NUMBER) & (just != 0u) & (rv == tn + 1)
+                                   : rc == QSMD_TICKET_OK);
                     stw = j;
-                    RS |= (tt ? 0u : 1u) << depth;     // transition: Reset => Just 0
+                    RS |= ((ok & !tt) ? 1u : 0u) << depth;   // transition: Reset => Just 0
                 }
-                stk.put(depth, stw);
-                ++depth;
+                // budget before the node is counted, then Map.! (rare exit)
+                const bool over = has & (nodes >= node_limit);
+                if (over | err) {
+                    status = over ? QSMD_STATUS_BUDGET : QSMD_STATUS_MODEL_ERROR;
+                    nodes += over ? 0u : 1u;
+                    break;
+                }
+                nodes += has ? 1u : 0u;
+                found = found | has;
+                // descend on success
+                stk.put(ok ? depth : 64u, stw);
+                depth += ok ? 1u : 0u;
                 const uint32_t fi = rem & pmj & INV;
-                rem &= ~((fi & (0u - fi)) | (1u << r));
-                cand = cands(rem, INV, RESP);
-                found = false;
+                const uint32_t rem2 = rem & ~((fi & (0u - fi)) | (1u << r));
+                rem = ok ? rem2 : rem;
+                cand = ok ? cands(rem2, INV, RESP) : cand;
+                found = found & !ok;
             }
         }
 

@@ -46,6 +46,7 @@ EXPORTS = {
     "qsmd_close": (None, [_P]),
     "qsmd_last_error": (ctypes.c_char_p, [_P]),
     "qsmd_set_time_limit_ms": (_I, [_P, _U64]),
+    "qsmd_set_stage0_grid": (_I, [_P, _U64]),
     "qsmd_check_batch": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P]),
     "qsmd_check_batch_device": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P, _P]),
     "qsmd_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
@@ -155,6 +156,9 @@ class Context:
         ms = ctypes.c_float()
         self._check(self._lib.qsmd_last_kernel_ms(self._h, ctypes.byref(ms)), "qsmd_last_kernel_ms")
         return float(ms.value)
+
+    def set_stage0_grid(self, max_blocks):
+        self._check(self._lib.qsmd_set_stage0_grid(self._h, int(max_blocks)), "qsmd_set_stage0_grid")
 
     def timing_reset(self):
         self._check(self._lib.qsmd_timing_reset(self._h), "qsmd_timing_reset")

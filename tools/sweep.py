@@ -1,0 +1,53 @@
+"""Interleaved A/B timing of search-kernel tuning knobs in ONE process
+(cdna_hip_programming.md §5.4 rule 24).  Usage on the GPU box:
+    python tools/sweep.py [--config bank_4x16] [--n 1000000] [--rounds 5]
+Prints, per variant, the median / min stage-0 kernel time over all rounds."""
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "quickcheck-state-machine-distributed_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from qsmd import device, gen  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="bank_4x16")
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--grids", default="1024,2048,4096,8192,16384,65536")
+    args = ap.parse_args()
+    cfg = gen.CONFIGS[args.config]
+    hdr, ev, _ = gen.generate_config(args.config, 0, args.n, threads=16)
+    dev = torch.device("cuda", 0)
+    d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
+    d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
+    d_st = torch.empty(args.n, dtype=torch.uint8, device=dev)
+    d_nd = torch.empty(args.n, dtype=torch.int64, device=dev)
+    ctx = device.Context(0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    grids = [int(g) for g in args.grids.split(",")]
+    res = {g: [] for g in grids}
+    for _ in range(args.rounds):
+        for g in grids:
+            ctx.set_stage0_grid(g)
+            ctx.timing_reset()
+            for _ in range(args.reps):
+                ctx.check_device(cfg["model_id"], d_hdr.data_ptr(), args.n, d_ev.data_ptr(), len(ev),
+                                 d_st.data_ptr(), d_nd.data_ptr(), None, None, stream=stream)
+            s0, _ = ctx.timing_read()
+            res[g].extend(float(x) for x in s0)
+    out = {str(g): {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))} for g, v in res.items()}
+    print(json.dumps({"config": args.config, "n": args.n, "stage0": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
