@@ -194,6 +194,12 @@ int qsmd_set_time_limit_ms(qsmd_ctx* ctx, uint64_t ms);
  * Default 65536.  Does not change any result. */
 int qsmd_set_stage0_grid(qsmd_ctx* ctx, uint64_t max_blocks);
 
+/* Diagnostic: when stamps_dev (device memory, 4 x u64 per stage-0
+ * workgroup) is non-NULL, stage 0 runs an instrumented build that records
+ * per-workgroup s_memtime totals of its phases (staging, search, output,
+ * groups processed).  NULL restores the production kernel. */
+int qsmd_diag_stamps(qsmd_ctx* ctx, void* stamps_dev);
+
 /* Device time (ms, HIP events on the launch stream) of the search kernels of
  * the most recent check call, measured once that stream has completed. */
 int qsmd_last_kernel_ms(qsmd_ctx* ctx, float* ms_out);

@@ -37,6 +37,7 @@ struct qsmd_ctx {
     bool timed = false;
     uint64_t time_limit_ms = 120000;   // safety net per search launch
     uint64_t stage0_max_grid = 65536;  // tuning: cap on stage-0 workgroups (grid-stride beyond)
+    unsigned long long* stamps = nullptr;   // diagnostic: stage-0 phase timings
 };
 
 namespace {
@@ -150,6 +151,12 @@ void qsmd_close(qsmd_ctx* c) {
     delete c;
 }
 
+int qsmd_diag_stamps(qsmd_ctx* c, void* stamps_dev) {
+    if (!c) return QSMD_ERR_ARG;
+    c->stamps = static_cast<unsigned long long*>(stamps_dev);
+    return QSMD_OK;
+}
+
 int qsmd_set_stage0_grid(qsmd_ctx* c, uint64_t max_blocks) {
     if (!c || max_blocks == 0 || max_blocks > 0x7FFFFFFFull) return QSMD_ERR_ARG;
     c->stage0_max_grid = max_blocks;
@@ -219,6 +226,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.defer_list = l0;
     a0.defer_count = cnt + 0;
     a0.partials = part;
+    a0.stamps = c->stamps;
     HIP_TRY(c, launch_compact(a0, (uint32_t)g0, s), "stage 0 launch");
     HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
     // stage 1: histories with 33..64 events

@@ -128,7 +128,9 @@ struct Stack16 {
 
 }  // namespace
 
-template <uint32_t MODEL>
+// STAMP = diagnostic build: lane 0 accumulates s_memtime deltas of the
+// phases (header+staging, search, output) into a.stamps[block][4].
+template <uint32_t MODEL, bool STAMP>
 __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
     constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
     __shared__ uint32_t s_ev[C_MAXEV][C_LANES];
@@ -140,9 +142,11 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
     uint64_t c_nodes = 0;
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t node_limit = a.max_nodes ? a.max_nodes : ~0ull;
+    uint64_t st_acc[4] = {0, 0, 0, 0}, ts_a = 0, ts_b = 0;
 
     for (uint64_t base = (uint64_t)blockIdx.x * C_LANES; base < total;
          base += (uint64_t)gridDim.x * C_LANES) {
+        if constexpr (STAMP) ts_a = __builtin_amdgcn_s_memtime();
         const uint64_t idx = base + lane;
         const bool active = idx < total;
         const uint32_t h = (uint32_t)idx;
@@ -200,6 +204,10 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
             return ~((P0 ^ m0) | (P1 ^ m1) | (P2 ^ m2)) & ALL;
         };
         const bool defer = enc_ok && (!small || (ok && !fits));
+        if constexpr (STAMP) {
+            ts_b = __builtin_amdgcn_s_memtime();
+            st_acc[0] += ts_b - ts_a;
+        }
 
         // ---- overflow to stage 1 (wave-aggregated append)
         const uint64_t dm = __ballot(defer);
@@ -363,6 +371,10 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
                 found = found & !ok;
             }
         }
+        if constexpr (STAMP) {
+            ts_a = __builtin_amdgcn_s_memtime();
+            st_acc[1] += ts_a - ts_b;
+        }
 
         a.status[h] = (uint8_t)status;
         if (a.nodes) a.nodes[h] = nodes;
@@ -377,6 +389,16 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
         c_enc += status == QSMD_STATUS_ENCODE_ERROR;
         c_budget += status == QSMD_STATUS_BUDGET;
         c_nodes += nodes;
+        if constexpr (STAMP) {
+            st_acc[2] += __builtin_amdgcn_s_memtime() - ts_a;
+            st_acc[3] += 1;
+        }
+    }
+    if constexpr (STAMP) {
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) a.stamps[(uint64_t)blockIdx.x * 4 + k] = st_acc[k];
+        }
     }
 
     const uint64_t t_lin = wave_sum64(c_lin), t_non = wave_sum64(c_nonlin), t_err = wave_sum64(c_err),
@@ -395,10 +417,14 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
 }
 
 hipError_t launch_compact(const SearchArgs& a, uint32_t grid, hipStream_t s) {
-    if (a.model_id == QSMD_MODEL_BANK)
-        hipLaunchKernelGGL(compact_search<QSMD_MODEL_BANK>, dim3(grid), dim3(C_LANES), 0, s, a);
-    else
-        hipLaunchKernelGGL(compact_search<QSMD_MODEL_TICKET>, dim3(grid), dim3(C_LANES), 0, s, a);
+    const bool bank = a.model_id == QSMD_MODEL_BANK;
+    if (a.stamps) {
+        if (bank) hipLaunchKernelGGL((compact_search<QSMD_MODEL_BANK, true>), dim3(grid), dim3(C_LANES), 0, s, a);
+        else hipLaunchKernelGGL((compact_search<QSMD_MODEL_TICKET, true>), dim3(grid), dim3(C_LANES), 0, s, a);
+    } else {
+        if (bank) hipLaunchKernelGGL((compact_search<QSMD_MODEL_BANK, false>), dim3(grid), dim3(C_LANES), 0, s, a);
+        else hipLaunchKernelGGL((compact_search<QSMD_MODEL_TICKET, false>), dim3(grid), dim3(C_LANES), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -38,6 +38,7 @@ struct SearchArgs {
     uint8_t* witness;             // may be null
     unsigned long long* partials; // [gridDim.x][T_N]
     uint32_t* timed_out;          // set to 1 if the time limit fired
+    unsigned long long* stamps;   // diagnostic phase timings (null in production)
 };
 
 // Stage 0 (csrc/compact.hip): <= 32 events, <= 8 pids, 19-bit values.

@@ -47,6 +47,7 @@ EXPORTS = {
     "qsmd_last_error": (ctypes.c_char_p, [_P]),
     "qsmd_set_time_limit_ms": (_I, [_P, _U64]),
     "qsmd_set_stage0_grid": (_I, [_P, _U64]),
+    "qsmd_diag_stamps": (_I, [_P, _P]),
     "qsmd_check_batch": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P]),
     "qsmd_check_batch_device": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P, _P]),
     "qsmd_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
@@ -159,6 +160,9 @@ class Context:
 
     def set_stage0_grid(self, max_blocks):
         self._check(self._lib.qsmd_set_stage0_grid(self._h, int(max_blocks)), "qsmd_set_stage0_grid")
+
+    def diag_stamps(self, ptr):
+        self._check(self._lib.qsmd_diag_stamps(self._h, ptr), "qsmd_diag_stamps")
 
     def timing_reset(self):
         self._check(self._lib.qsmd_timing_reset(self._h), "qsmd_timing_reset")

@@ -46,7 +46,26 @@ def main():
             s0, _ = ctx.timing_read()
             res[g].extend(float(x) for x in s0)
     out = {str(g): {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))} for g, v in res.items()}
-    print(json.dumps({"config": args.config, "n": args.n, "stage0": out}, indent=1))
+    # diagnostic build: per-phase s_memtime cycles per 64-history group
+    g0 = min((args.n + 63) // 64, 65536)
+    st = torch.zeros(g0 * 4, dtype=torch.int64, device=dev)
+    ctx.set_stage0_grid(65536)
+    ctx.diag_stamps(st.data_ptr())
+    ctx.timing_reset()
+    ctx.check_device(cfg["model_id"], d_hdr.data_ptr(), args.n, d_ev.data_ptr(), len(ev),
+                     d_st.data_ptr(), d_nd.data_ptr(), None, None, stream=stream)
+    s0, _ = ctx.timing_read()
+    ctx.diag_stamps(None)
+    stamps = st.view(g0, 4).cpu().numpy().astype(np.float64)
+    groups = stamps[:, 3].sum()
+    nd = d_nd.cpu().numpy()
+    diag = {"stamped_kernel_ms": float(s0[0]),
+            "cycles_per_group": {"stage": stamps[:, 0].sum() / groups, "search": stamps[:, 1].sum() / groups,
+                                 "output": stamps[:, 2].sum() / groups},
+            "search_cycles_p50_p90_max": [float(np.percentile(stamps[:, 1], q)) for q in (50, 90, 100)],
+            "nodes_mean": float(nd.mean()), "nodes_group_max_mean": float(nd.reshape(-1, 64).max(1).mean())
+            if args.n % 64 == 0 else None}
+    print(json.dumps({"config": args.config, "n": args.n, "stage0": out, "diag": diag}, indent=1))
 
 
 if __name__ == "__main__":
