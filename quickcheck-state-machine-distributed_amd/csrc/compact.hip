@@ -135,6 +135,7 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
     constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
     __shared__ uint32_t s_ev[C_MAXEV][C_LANES];
     __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
+    __shared__ uint32_t s_flag[C_LANES];
 
     const int lane = threadIdx.x;
     const uint64_t total = a.n_hist;
@@ -158,12 +159,87 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
                             n_pid <= QSMD_MAX_PIDS && (uint64_t)H.ev_off + n_ev <= a.n_events;
         const bool small = enc_ok && n_ev <= (uint32_t)C_MAXEV && n_pid <= 8u && a.m0_small;
 
-        // ---- stage: C_CHUNK loads in flight (index clamped into the
-        //      history), then compress into LDS and build the register masks.
-        //      Pids are bit-sliced: P0/P1/P2 hold bit 0/1/2 of each event's pid.
+        // ---- stage the 64 histories into LDS as compressed u32 [event][lane]
+        //      and build the per-lane register masks.  Pids are bit-sliced:
+        //      P0/P1/P2 hold bit 0/1/2 of each event's pid.
         uint32_t INV = 0, RESP = 0, P0 = 0, P1 = 0, P2 = 0;
         bool ok = enc_ok, fits = small;
-        if (small && n_ev > 0) {
+        // Fast path: the wave's histories are packed back to back with one
+        // common length N (the layout every batch builder here produces).
+        // Then the whole 64*N-event block is read with fully coalesced
+        // 16-byte loads (a per-lane history walk touches 64 cache lines per
+        // wave instruction and leaves the vector L1 address-bound), each
+        // loaded event is validated, compressed and scattered to its
+        // history's lane slot, and every lane then builds its masks from LDS.
+        const uint32_t N0 = __builtin_amdgcn_readfirstlane(n_ev);
+        const uint32_t off0 = __builtin_amdgcn_readfirstlane(H.ev_off);
+        const bool lane_uni = active && small && n_ev == N0 && H.ev_off == off0 + (uint32_t)lane * N0;
+        const bool packed = __ballot(!lane_uni) == 0ull && N0 > 0u;
+        if (packed) {
+            s_flag[lane] = 0u;
+            const float invN = 1.0f / (float)N0;
+            auto put_event = [&](uint32_t g, uint32_t lo, int32_t val) {
+                const uint32_t hh = (uint32_t)(((float)g + 0.5f) * invN);   // exact for g < 2^11
+                const uint32_t e = g - hh * N0;
+                const uint32_t p = lo & 0x7Fu;
+                const uint32_t np = (uint32_t)__shfl((int)n_pid, (int)hh, 64);
+                const bool vok = (p < np) & valid_bits<MODEL>(lo);
+                const bool vfit = (val >= V19_MIN) & (val <= V19_MAX);
+                s_ev[e][hh] = (p & 7u) | (((lo >> 7) & 1u) << 3) | (((lo >> 8) & 7u) << 4) |
+                              (((lo >> 16) & 7u) << 7) | (((lo >> 24) & 7u) << 10) |
+                              ((uint32_t)val << 13);
+                if (!(vok & vfit)) atomicOr(&s_flag[hh], vok ? 2u : 1u);
+            };
+            const uint32_t total_ev = 64u * N0;
+            if ((off0 & 1u) == 0u) {
+                const uint4* blk = reinterpret_cast<const uint4*>(a.events + off0);
+                for (uint32_t k0 = 0; k0 < total_ev / 2u; k0 += 4u * 64u) {
+                    uint4 x[4];
+#pragma unroll
+                    for (uint32_t u = 0; u < 4; ++u) {
+                        const uint32_t q = k0 + u * 64u + (uint32_t)lane;
+                        x[u] = q < total_ev / 2u ? blk[q] : make_uint4(0u, 0u, 0u, 0u);
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < 4; ++u) {
+                        const uint32_t q = k0 + u * 64u + (uint32_t)lane;
+                        if (q < total_ev / 2u) {
+                            put_event(2u * q, x[u].x, (int32_t)x[u].y);
+                            put_event(2u * q + 1u, x[u].z, (int32_t)x[u].w);
+                        }
+                    }
+                }
+            } else {
+                const uint2* blk = a.events + off0;
+                for (uint32_t k0 = 0; k0 < total_ev; k0 += 8u * 64u) {
+                    uint2 x[8];
+#pragma unroll
+                    for (uint32_t u = 0; u < 8; ++u) {
+                        const uint32_t g = k0 + u * 64u + (uint32_t)lane;
+                        x[u] = g < total_ev ? blk[g] : make_uint2(0u, 0u);
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < 8; ++u) {
+                        const uint32_t g = k0 + u * 64u + (uint32_t)lane;
+                        if (g < total_ev) put_event(g, x[u].x, (int32_t)x[u].y);
+                    }
+                }
+            }
+            const uint32_t fl = s_flag[lane];
+            ok = ok & ((fl & 1u) == 0u);
+            fits = fits & ((fl & 2u) == 0u);
+#pragma unroll
+            for (uint32_t e = 0; e < (uint32_t)C_MAXEV; ++e) {
+                const uint32_t cw = s_ev[e][lane];
+                const uint32_t bit = e < n_ev ? (1u << e) : 0u;
+                const uint32_t resp = (cw >> 3) & 1u;
+                RESP |= resp ? bit : 0u;
+                INV |= resp ? 0u : bit;
+                P0 |= (cw & 1u) ? bit : 0u;
+                P1 |= (cw & 2u) ? bit : 0u;
+                P2 |= (cw & 4u) ? bit : 0u;
+            }
+        } else if (small && n_ev > 0) {
             const uint2* evp = a.events + H.ev_off;
             const uint32_t last = n_ev - 1u;
 #pragma unroll

@@ -94,6 +94,28 @@ def test_stage_cascade(ctx, n_ev, n_pid):
         _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
 
 
+@pytest.mark.parametrize("model,n_ev", [("bank", 32), ("bank", 20), ("ticket", 24), ("ticket", 7)])
+def test_packed_uniform_batches(ctx, model, n_ev):
+    """Batches whose histories are packed back to back with one length take the
+    coalesced staging path; corrupt some events (encode errors) and widen some
+    values (deferral to stage 1) so every outcome goes through that path."""
+    rng = random.Random(n_ev * 7 + len(model))
+    m = models.BY_NAME[model]
+    hs = []
+    while len(hs) < 64 * 60:
+        h = histgen.wellformed_history(rng, model, n_ev // 2, rng.randint(1, 5), p_pending=0.0)
+        if len(h) >= n_ev:
+            hs.append(h[:n_ev])
+    b = codec.encode(m, hs)
+    ev = b.events.copy()
+    nr = np.random.default_rng(n_ev)
+    bad = nr.choice(len(ev), 40, replace=False)
+    ev["code"][bad[:20]] = 9                                   # unknown constructor
+    ev["val"][bad[20:]] = 1 << 20                              # > 19-bit: deferred
+    for hdr in (b.hdr, b.hdr[1:]):                             # even and odd block start
+        _compare(ctx, m.model_id, hdr, ev, max_nodes=200000)
+
+
 def test_mixed_sizes_one_batch(ctx):
     rng = random.Random(7)
     hs = []
