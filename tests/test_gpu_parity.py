@@ -103,7 +103,7 @@ def test_packed_uniform_batches(ctx, model, n_ev):
     m = models.BY_NAME[model]
     hs = []
     while len(hs) < 64 * 60:
-        h = histgen.wellformed_history(rng, model, n_ev // 2, rng.randint(1, 5), p_pending=0.0)
+        h = histgen.wellformed_history(rng, model, (n_ev + 1) // 2, rng.randint(1, 5), p_pending=0.0)
         if len(h) >= n_ev:
             hs.append(h[:n_ev])
     b = codec.encode(m, hs)
