@@ -178,11 +178,18 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
         if (packed) {
             s_flag[lane] = 0u;
             const float invN = 1.0f / (float)N0;
-            auto put_event = [&](uint32_t g, uint32_t lo, int32_t val) {
-                const uint32_t hh = (uint32_t)(((float)g + 0.5f) * invN);   // exact for g < 2^11
+            // history of block event g (exact for g < 2^11)
+            auto hist_of = [&](uint32_t g) -> uint32_t {
+                return (uint32_t)(((float)g + 0.5f) * invN) & 63u;
+            };
+            // n_pid of that history: the cross-lane read runs with every lane
+            // active (ds_bpermute from an inactive source lane returns 0)
+            auto npid_of = [&](uint32_t hh) -> uint32_t {
+                return (uint32_t)__shfl((int)n_pid, (int)hh, 64);
+            };
+            auto put_event = [&](uint32_t g, uint32_t hh, uint32_t np, uint32_t lo, int32_t val) {
                 const uint32_t e = g - hh * N0;
                 const uint32_t p = lo & 0x7Fu;
-                const uint32_t np = (uint32_t)__shfl((int)n_pid, (int)hh, 64);
                 const bool vok = (p < np) & valid_bits<MODEL>(lo);
                 const bool vfit = (val >= V19_MIN) & (val <= V19_MAX);
                 s_ev[e][hh] = (p & 7u) | (((lo >> 7) & 1u) << 3) | (((lo >> 8) & 7u) << 4) |
@@ -203,9 +210,11 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
 #pragma unroll
                     for (uint32_t u = 0; u < 4; ++u) {
                         const uint32_t q = k0 + u * 64u + (uint32_t)lane;
+                        const uint32_t h0 = hist_of(2u * q), h1 = hist_of(2u * q + 1u);
+                        const uint32_t np0 = npid_of(h0), np1 = npid_of(h1);
                         if (q < total_ev / 2u) {
-                            put_event(2u * q, x[u].x, (int32_t)x[u].y);
-                            put_event(2u * q + 1u, x[u].z, (int32_t)x[u].w);
+                            put_event(2u * q, h0, np0, x[u].x, (int32_t)x[u].y);
+                            put_event(2u * q + 1u, h1, np1, x[u].z, (int32_t)x[u].w);
                         }
                     }
                 }
@@ -221,7 +230,9 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
 #pragma unroll
                     for (uint32_t u = 0; u < 8; ++u) {
                         const uint32_t g = k0 + u * 64u + (uint32_t)lane;
-                        if (g < total_ev) put_event(g, x[u].x, (int32_t)x[u].y);
+                        const uint32_t hh = hist_of(g);
+                        const uint32_t np = npid_of(hh);
+                        if (g < total_ev) put_event(g, hh, np, x[u].x, (int32_t)x[u].y);
                     }
                 }
             }
