@@ -1,0 +1,88 @@
+"""The N>1 path on CPU: world_size-2 gloo processes each check their own
+contiguous shard of one seeded stream and all-reduce the counters; the result
+must equal one process checking the whole stream.  (On the GPUs the same code
+runs with the nccl = RCCL backend and the HIP checker; here the per-rank
+checker is the C oracle, so only the sharding/collective logic is under test.)"""
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _oracle_checker(model_id, hdr, events):
+    import oracle_c
+    st, nd, _ = oracle_c.check_batch(model_id, hdr, events, threads=2, max_nodes=10**6)
+    return st, nd
+
+
+def _worker(rank, world, port, config, n_total, out_q):
+    sys.path[:0] = [os.path.join(HERE, "..", "quickcheck-state-machine-distributed_amd"),
+                    os.path.join(HERE, "..", "oracle"), HERE]
+    import torch.distributed as dist
+
+    from qsmd import dist as qdist
+    from qsmd import gen
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        p = gen.params(**gen.CONFIGS[config])
+        tot, stop, (first, count), st, nd = qdist.check_sharded(_oracle_checker, p, n_total, rank, world)
+        out_q.put((rank, tot.tolist(), stop, first, count, st.tolist(), [int(x) for x in nd]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_partition():
+    from qsmd.dist import shard
+    for n in (0, 1, 7, 64, 1000, 1001):
+        for w in (1, 2, 3, 8):
+            parts = [shard(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0
+            assert sum(c for _, c in parts) == n
+            for (f0, c0), (f1, _) in zip(parts, parts[1:]):
+                assert f0 + c0 == f1
+
+
+@pytest.mark.parametrize("config", ["bank_4x16_bugs", "ticket_2x10"])
+def test_two_rank_gloo_equals_single_process(config):
+    from qsmd import dist as qdist
+    from qsmd import gen
+
+    world, n_total = 2, 3001
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, config, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    results.sort()
+    # every rank holds the same global totals
+    assert results[0][1] == results[1][1] and results[0][2] == results[1][2]
+    # single-process reference over the whole stream
+    hdr, ev, _ = gen.generate(gen.params(**gen.CONFIGS[config]), 0, n_total)
+    st, nd = _oracle_checker(gen.CONFIGS[config]["model_id"], hdr, ev)
+    assert results[0][1] == qdist.totals_from_status(st, nd).tolist()
+    cat_st = np.array(results[0][5] + results[1][5])
+    cat_nd = np.array(results[0][6] + results[1][6])
+    assert np.array_equal(cat_st, st) and np.array_equal(cat_nd, nd.astype(np.int64))
+    assert results[0][2] == int((st == 0).any() or (st == 2).any())
