@@ -38,12 +38,14 @@ struct qsmd_ctx {
     uint64_t time_limit_ms = 120000;   // safety net per search launch
     uint64_t stage0_max_grid = 65536;  // tuning: cap on stage-0 workgroups (grid-stride beyond)
     unsigned long long* stamps = nullptr;   // diagnostic: stage-0 phase timings
+    uint64_t stage0_budget = 64;       // stage-0 node budget before the refill stage (0 = none)
 };
 
 namespace {
 
 constexpr uint32_t kStage1Grid = 1024;   // list-mode stages: grid-stride
 constexpr uint32_t kStage2Grid = 1024;
+constexpr uint32_t kRefillGrid = 2048;   // persistent: 8 wavefronts per CU
 constexpr uint64_t kTimingSlots = 1024;
 
 int fail(qsmd_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
@@ -157,6 +159,12 @@ int qsmd_diag_stamps(qsmd_ctx* c, void* stamps_dev) {
     return QSMD_OK;
 }
 
+int qsmd_set_stage0_budget(qsmd_ctx* c, uint64_t nodes) {
+    if (!c) return QSMD_ERR_ARG;
+    c->stage0_budget = nodes;
+    return QSMD_OK;
+}
+
 int qsmd_set_stage0_grid(qsmd_ctx* c, uint64_t max_blocks) {
     if (!c || max_blocks == 0 || max_blocks > 0x7FFFFFFFull) return QSMD_ERR_ARG;
     c->stage0_max_grid = max_blocks;
@@ -186,12 +194,16 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
 
     // ---- workspace: defer lists, counters, partials, internal totals
     const uint64_t g0 = std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), c->stage0_max_grid);
-    const uint64_t n_part = g0 + kStage1Grid + kStage2Grid;
-    const size_t off_cnt = 0;                                          // 4 x u32
+    const uint64_t g0b = kRefillGrid;
+    const uint64_t n_part = g0 + g0b + kStage1Grid + kStage2Grid;
+    // counters: [0] stage-1 list, [1] stage-2 list, [2] timed out, [3] unused,
+    //           [4] heavy list, [5] heavy queue head
+    const size_t off_cnt = 0;
     const size_t off_tot = 256;                                        // qsmd_totals
     const size_t off_l0 = 512;
     const size_t off_l1 = off_l0 + align_up(n_hist * 4 + 4);
-    const size_t off_part = off_l1 + align_up(n_hist * 4 + 4);
+    const size_t off_lh = off_l1 + align_up(n_hist * 4 + 4);
+    const size_t off_part = off_lh + align_up(n_hist * 4 + 4);
     const size_t need = off_part + align_up(n_part * T_N * 8);
     rc = grow(c, &c->ws, &c->ws_bytes, need);
     if (rc) return rc;
@@ -199,9 +211,10 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     qsmd_totals* tot = totals ? totals : reinterpret_cast<qsmd_totals*>(c->ws + off_tot);
     uint32_t* l0 = reinterpret_cast<uint32_t*>(c->ws + off_l0);
     uint32_t* l1 = reinterpret_cast<uint32_t*>(c->ws + off_l1);
+    uint32_t* lh = reinterpret_cast<uint32_t*>(c->ws + off_lh);
     unsigned long long* part = reinterpret_cast<unsigned long long*>(c->ws + off_part);
 
-    HIP_TRY(c, hipMemsetAsync(cnt, 0, 16, s), "memset counters");
+    HIP_TRY(c, hipMemsetAsync(cnt, 0, 32, s), "memset counters");
     HIP_TRY(c, hipMemsetAsync(tot, 0, sizeof(qsmd_totals), s), "memset totals");
 
     a.hdr = hdr;
@@ -227,15 +240,25 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.defer_count = cnt + 0;
     a0.partials = part;
     a0.stamps = c->stamps;
+    a0.heavy_list = c->stage0_budget ? lh : nullptr;
+    a0.heavy_count = cnt + 4;
+    a0.stage0_budget = c->stage0_budget;
     HIP_TRY(c, launch_compact(a0, (uint32_t)g0, s), "stage 0 launch");
     HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
+    // stage 0b: histories over the stage-0 node budget, persistent refill
+    SearchArgs ab = a;
+    ab.list = lh;
+    ab.list_count = cnt + 4;
+    ab.queue_head = cnt + 5;
+    ab.partials = part + g0 * T_N;
+    HIP_TRY(c, launch_refill(ab, (uint32_t)g0b, s), "stage 0b launch");
     // stage 1: histories with 33..64 events
     SearchArgs a1 = a;
     a1.list = l0;
     a1.list_count = cnt + 0;
     a1.defer_list = l1;
     a1.defer_count = cnt + 1;
-    a1.partials = part + g0 * T_N;
+    a1.partials = part + (g0 + g0b) * T_N;
     HIP_TRY(c, launch_stage(1, a1, kStage1Grid, s), "stage 1 launch");
     // stage 2: up to 128 events / 128 pids
     SearchArgs a2 = a;
@@ -243,7 +266,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a2.list_count = cnt + 1;
     a2.defer_list = l0;            // never written: stage 2 holds every valid history
     a2.defer_count = cnt + 3;
-    a2.partials = part + (g0 + kStage1Grid) * T_N;
+    a2.partials = part + (g0 + g0b + kStage1Grid) * T_N;
     HIP_TRY(c, launch_stage(2, a2, kStage2Grid, s), "stage 2 launch");
     HIP_TRY(c, launch_reduce(part, n_part, tot, s), "reduce launch");
     HIP_TRY(c, hipEventRecord(evs[2], s), "hipEventRecord");

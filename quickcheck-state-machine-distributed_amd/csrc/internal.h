@@ -23,6 +23,13 @@ struct SearchArgs {
     // overflow: histories this stage cannot hold go to defer_list
     uint32_t* defer_list;
     uint32_t* defer_count;
+    // stage 0: histories over the stage-0 node budget go to heavy_list
+    // (searched again from scratch by the refill stage, whose queue head is
+    // queue_head); null heavy_list = no stage-0 budget
+    uint32_t* heavy_list;
+    uint32_t* heavy_count;
+    uint32_t* queue_head;
+    uint64_t stage0_budget;
     uint32_t flags;
     uint32_t model_id;
     uint64_t max_nodes;           // 0 = unbounded
@@ -43,6 +50,8 @@ struct SearchArgs {
 
 // Stage 0 (csrc/compact.hip): <= 32 events, <= 8 pids, 19-bit values.
 hipError_t launch_compact(const SearchArgs& a, uint32_t grid, hipStream_t s);
+// Stage 0b (csrc/compact.hip): persistent refill search over the heavy list.
+hipError_t launch_refill(const SearchArgs& a, uint32_t grid, hipStream_t s);
 // Stages 1 and 2 (csrc/search.hip): list mode over the deferred histories.
 hipError_t launch_stage(int stage, const SearchArgs& a, uint32_t grid, hipStream_t s);
 uint32_t stage_lanes(int stage);

@@ -47,6 +47,7 @@ EXPORTS = {
     "qsmd_last_error": (ctypes.c_char_p, [_P]),
     "qsmd_set_time_limit_ms": (_I, [_P, _U64]),
     "qsmd_set_stage0_grid": (_I, [_P, _U64]),
+    "qsmd_set_stage0_budget": (_I, [_P, _U64]),
     "qsmd_diag_stamps": (_I, [_P, _P]),
     "qsmd_check_batch": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P]),
     "qsmd_check_batch_device": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P, _P]),
@@ -160,6 +161,9 @@ class Context:
 
     def set_stage0_grid(self, max_blocks):
         self._check(self._lib.qsmd_set_stage0_grid(self._h, int(max_blocks)), "qsmd_set_stage0_grid")
+
+    def set_stage0_budget(self, nodes):
+        self._check(self._lib.qsmd_set_stage0_budget(self._h, int(nodes)), "qsmd_set_stage0_budget")
 
     def diag_stamps(self, ptr):
         self._check(self._lib.qsmd_diag_stamps(self._h, ptr), "qsmd_diag_stamps")

@@ -23,7 +23,9 @@ def main():
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--grids", default="1024,2048,4096,8192,16384,65536")
+    ap.add_argument("--grids", default="65536")
+    ap.add_argument("--budgets", default="64", help="stage-0 node budgets (0 = none)")
+    ap.add_argument("--no-stamps", action="store_true")
     args = ap.parse_args()
     cfg = gen.CONFIGS[args.config]
     hdr, ev, _ = gen.generate_config(args.config, 0, args.n, threads=16)
@@ -34,22 +36,30 @@ def main():
     d_nd = torch.empty(args.n, dtype=torch.int64, device=dev)
     ctx = device.Context(0)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    grids = [int(g) for g in args.grids.split(",")]
-    res = {g: [] for g in grids}
+    variants = [(int(g), int(b)) for g in args.grids.split(",") for b in args.budgets.split(",")]
+    res = {v: ([], []) for v in variants}
     for _ in range(args.rounds):
-        for g in grids:
+        for g, b in variants:
             ctx.set_stage0_grid(g)
+            ctx.set_stage0_budget(b)
             ctx.timing_reset()
             for _ in range(args.reps):
                 ctx.check_device(cfg["model_id"], d_hdr.data_ptr(), args.n, d_ev.data_ptr(), len(ev),
                                  d_st.data_ptr(), d_nd.data_ptr(), None, None, stream=stream)
-            s0, _ = ctx.timing_read()
-            res[g].extend(float(x) for x in s0)
-    out = {str(g): {"median_ms": float(np.median(v)), "min_ms": float(np.min(v))} for g, v in res.items()}
+            s0, call = ctx.timing_read()
+            res[(g, b)][0].extend(float(x) for x in s0)
+            res[(g, b)][1].extend(float(x) for x in call)
+    out = {f"grid{g}_budget{b}": {"stage0_median_ms": float(np.median(v[0])),
+                                  "call_median_ms": float(np.median(v[1])),
+                                  "call_min_ms": float(np.min(v[1]))} for (g, b), v in res.items()}
+    if args.no_stamps:
+        print(json.dumps({"config": args.config, "n": args.n, "variants": out}, indent=1))
+        return
     # diagnostic build: per-phase s_memtime cycles per 64-history group
     g0 = min((args.n + 63) // 64, 65536)
     st = torch.zeros(g0 * 4, dtype=torch.int64, device=dev)
     ctx.set_stage0_grid(65536)
+    ctx.set_stage0_budget(0)
     ctx.diag_stamps(st.data_ptr())
     ctx.timing_reset()
     ctx.check_device(cfg["model_id"], d_hdr.data_ptr(), args.n, d_ev.data_ptr(), len(ev),
@@ -65,7 +75,7 @@ def main():
             "search_cycles_p50_p90_max": [float(np.percentile(stamps[:, 1], q)) for q in (50, 90, 100)],
             "nodes_mean": float(nd.mean()), "nodes_group_max_mean": float(nd.reshape(-1, 64).max(1).mean())
             if args.n % 64 == 0 else None}
-    print(json.dumps({"config": args.config, "n": args.n, "stage0": out, "diag": diag}, indent=1))
+    print(json.dumps({"config": args.config, "n": args.n, "variants": out, "diag": diag}, indent=1))
 
 
 if __name__ == "__main__":
