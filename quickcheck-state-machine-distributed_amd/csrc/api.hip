@@ -185,8 +185,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         return fail(c, QSMD_ERR_ARG, "unknown model_id");
     if (n_hist && (!hdr || !status)) return fail(c, QSMD_ERR_ARG, "null hdr/status");
     if (n_hist > 0xFFFFFFFFull) return fail(c, QSMD_ERR_ARG, "n_hist > 2^32-1");
-    if (flags & QSMD_FLAG_EARLY_EXIT_BATCH)
-        return fail(c, QSMD_ERR_UNSUPPORTED, "EARLY_EXIT_BATCH not implemented yet");
+    const bool early = (flags & QSMD_FLAG_EARLY_EXIT_BATCH) != 0;
     SearchArgs a{};
     int rc = fill_model0(c, model_id, model0, a);
     if (rc) return rc;
@@ -195,15 +194,17 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // ---- workspace: defer lists, counters, partials, internal totals
     const uint64_t g0 = std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), c->stage0_max_grid);
     const uint64_t g0b = kRefillGrid;
-    const uint64_t n_part = g0 + g0b + kStage1Grid + kStage2Grid;
+    const uint64_t gfx = early ? std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), 4096) : 0;
+    const uint64_t n_part = g0 + g0b + kStage1Grid + kStage2Grid + gfx;
     // counters: [0] stage-1 list, [1] stage-2 list, [2] timed out, [3] unused,
-    //           [4] heavy list, [5] heavy queue head
+    //           [4] heavy list, [5] heavy queue head, [6] first failing history
     const size_t off_cnt = 0;
     const size_t off_tot = 256;                                        // qsmd_totals
     const size_t off_l0 = 512;
     const size_t off_l1 = off_l0 + align_up(n_hist * 4 + 4);
     const size_t off_lh = off_l1 + align_up(n_hist * 4 + 4);
-    const size_t off_part = off_lh + align_up(n_hist * 4 + 4);
+    const size_t off_nd = off_lh + align_up(n_hist * 4 + 4);          // nodes if the caller has none
+    const size_t off_part = off_nd + (early && !nodes ? align_up(n_hist * 8) : 0);
     const size_t need = off_part + align_up(n_part * T_N * 8);
     rc = grow(c, &c->ws, &c->ws_bytes, need);
     if (rc) return rc;
@@ -213,9 +214,12 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     uint32_t* l1 = reinterpret_cast<uint32_t*>(c->ws + off_l1);
     uint32_t* lh = reinterpret_cast<uint32_t*>(c->ws + off_lh);
     unsigned long long* part = reinterpret_cast<unsigned long long*>(c->ws + off_part);
+    if (early && !nodes) nodes = reinterpret_cast<uint64_t*>(c->ws + off_nd);
 
     HIP_TRY(c, hipMemsetAsync(cnt, 0, 32, s), "memset counters");
+    HIP_TRY(c, hipMemsetAsync(cnt + 6, 0xFF, 4, s), "memset first_fail");
     HIP_TRY(c, hipMemsetAsync(tot, 0, sizeof(qsmd_totals), s), "memset totals");
+    a.first_fail = early ? cnt + 6 : nullptr;
 
     a.hdr = hdr;
     a.events = reinterpret_cast<const uint2*>(events);
@@ -268,7 +272,13 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a2.defer_count = cnt + 3;
     a2.partials = part + (g0 + g0b + kStage1Grid) * T_N;
     HIP_TRY(c, launch_stage(2, a2, kStage2Grid, s), "stage 2 launch");
-    HIP_TRY(c, launch_reduce(part, n_part, tot, s), "reduce launch");
+    if (early) {
+        unsigned long long* pf = part + (g0 + g0b + kStage1Grid + kStage2Grid) * T_N;
+        HIP_TRY(c, launch_early_exit_fixup(status, nodes, n_hist, cnt + 6, pf, (uint32_t)gfx, s), "fixup launch");
+        HIP_TRY(c, launch_reduce(pf, gfx, tot, s), "reduce launch");
+    } else {
+        HIP_TRY(c, launch_reduce(part, n_part, tot, s), "reduce launch");
+    }
     HIP_TRY(c, hipEventRecord(evs[2], s), "hipEventRecord");
     c->n_calls++;
     c->timed = true;

@@ -446,6 +446,7 @@ struct Counters {
     uint32_t lin = 0, nonlin = 0, err = 0, enc = 0, budget = 0;
     uint64_t nodes = 0;
     __device__ __forceinline__ void add(int status, uint64_t n) {
+        if (status == QSMD_STATUS_SKIPPED) return;     // counted by early_exit_fixup
         lin += status == QSMD_STATUS_LINEARISABLE;
         nonlin += status == QSMD_STATUS_NONLINEARISABLE;
         err += status == QSMD_STATUS_MODEL_ERROR;
@@ -530,10 +531,16 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
             status = QSMD_STATUS_ENCODE_ERROR;
         } else if (n_ev == 0) {
             status = QSMD_STATUS_LINEARISABLE;                       // :59
+        } else if (beyond_first_fail(a, h)) {
+            status = QSMD_STATUS_SKIPPED;
         } else {
             dfs.init(s, a, s_bal, lane);
             uint32_t iter = 0;
             while ((status = dfs.step(a, s_ev, s_bal, lane, limit)) < 0) {
+                if (((iter + 1u) & 1023u) == 0u && beyond_first_fail(a, h)) {
+                    status = QSMD_STATUS_SKIPPED;
+                    break;
+                }
                 if (time_up(a, t0, iter)) {
                     atomicOr(a.timed_out, 1u);
                     status = QSMD_STATUS_BUDGET;
@@ -541,6 +548,7 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
                 }
             }
         }
+        note_failure(a, h, status);
         if constexpr (STAMP) {
             ts_a = __builtin_amdgcn_s_memtime();
             st_acc[1] += ts_a - ts_b;
@@ -603,7 +611,7 @@ __global__ __launch_bounds__(C_LANES) void refill_search(SearchArgs a) {
             if (first + want >= count) exhausted = true;
             if (!busy) {
                 const uint32_t idx = first + lane_prefix(idle);
-                if (idx < count) {
+                if (idx < count && !beyond_first_fail(a, a.list[idx])) {   // else: early_exit_fixup
                     h = a.list[idx];
                     const qsmd_hdr H = a.hdr[h];
                     n_ev = H.n_ev;
@@ -618,11 +626,14 @@ __global__ __launch_bounds__(C_LANES) void refill_search(SearchArgs a) {
         if (__ballot(busy) == 0) break;
         if (busy) {
             int status = dfs.step(a, s_ev, s_bal, lane, limit);
+            if (status < 0 && ((iter + 1u) & 1023u) == 0u && beyond_first_fail(a, h))
+                status = QSMD_STATUS_SKIPPED;
             if (status < 0 && time_up(a, t0, iter)) {
                 atomicOr(a.timed_out, 1u);
                 status = QSMD_STATUS_BUDGET;
             }
             if (status >= 0) {
+                note_failure(a, h, status);
                 a.status[h] = (uint8_t)status;
                 if (a.nodes) a.nodes[h] = dfs.nodes;
                 if (a.witness && status == QSMD_STATUS_LINEARISABLE) dfs.write_witness(a.witness + ev_off, n_ev);

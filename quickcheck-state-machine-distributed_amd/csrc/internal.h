@@ -46,7 +46,23 @@ struct SearchArgs {
     unsigned long long* partials; // [gridDim.x][T_N]
     uint32_t* timed_out;          // set to 1 if the time limit fired
     unsigned long long* stamps;   // diagnostic phase timings (null in production)
+    // QSMD_FLAG_EARLY_EXIT_BATCH: smallest index of a history found
+    // non-linearisable (or raising); histories above it may stop early and
+    // are reported SKIPPED by early_exit_fixup.  Null when the flag is off.
+    uint32_t* first_fail;
 };
+
+// Early exit: relaxed agent-scope read (a stale value only delays skipping).
+__device__ __forceinline__ bool beyond_first_fail(const SearchArgs& a, uint32_t h) {
+    return a.first_fail && h > __hip_atomic_load(a.first_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void note_failure(const SearchArgs& a, uint32_t h, int status) {
+    if (a.first_fail && (status == QSMD_STATUS_NONLINEARISABLE || status == QSMD_STATUS_MODEL_ERROR))
+        atomicMin(a.first_fail, h);
+}
+
+hipError_t launch_early_exit_fixup(uint8_t* status, uint64_t* nodes, uint64_t n, const uint32_t* first_fail,
+                                   unsigned long long* partials, uint32_t grid, hipStream_t s);
 
 // Stage 0 (csrc/compact.hip): <= 32 events, <= 8 pids, 19-bit values.
 hipError_t launch_compact(const SearchArgs& a, uint32_t grid, hipStream_t s);

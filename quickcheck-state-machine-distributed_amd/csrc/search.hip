@@ -125,6 +125,8 @@ __global__ __launch_bounds__(LANES) void lane_search(SearchArgs a) {
             status = QSMD_STATUS_ENCODE_ERROR;
         } else if (n_ev == 0) {
             status = QSMD_STATUS_LINEARISABLE;                     // :59
+        } else if (beyond_first_fail(a, h)) {
+            status = QSMD_STATUS_SKIPPED;                          // early exit
         } else {
             // ---- model0
             BankState bank{a.m0_exists, 0u};
@@ -188,11 +190,13 @@ __global__ __launch_bounds__(LANES) void lane_search(SearchArgs a) {
                     found = true;
                     continue;
                 }
-                if (a.time_limit && ((++iter & 1023u) == 0u) &&
-                    __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
-                    atomicOr(a.timed_out, 1u);
-                    status = QSMD_STATUS_BUDGET;
-                    break;
+                if (((++iter & 1023u) == 0u)) {
+                    if (beyond_first_fail(a, h)) { status = QSMD_STATUS_SKIPPED; break; }
+                    if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
+                        atomicOr(a.timed_out, 1u);
+                        status = QSMD_STATUS_BUDGET;
+                        break;
+                    }
                 }
                 // ---- next candidate of this level
                 const int j = Ops::ctz(cand);
@@ -259,6 +263,7 @@ __global__ __launch_bounds__(LANES) void lane_search(SearchArgs a) {
         }
 
         // ---- outputs
+        note_failure(a, h, status);
         a.status[h] = (uint8_t)status;
         if (a.nodes) a.nodes[h] = nodes;
         if (a.witness && status == QSMD_STATUS_LINEARISABLE) {
@@ -266,6 +271,7 @@ __global__ __launch_bounds__(LANES) void lane_search(SearchArgs a) {
             for (int d = 0; d < depth; ++d) w[d] = (uint8_t)(s_meta[d][lane] & 0xFFu);
             if ((uint32_t)depth < n_ev) w[depth] = QSMD_WITNESS_END;
         }
+        if (status == QSMD_STATUS_SKIPPED) continue;           // counted by early_exit_fixup
         c_lin += status == QSMD_STATUS_LINEARISABLE;
         c_nonlin += status == QSMD_STATUS_NONLINEARISABLE;
         c_err += status == QSMD_STATUS_MODEL_ERROR;
@@ -289,6 +295,43 @@ __global__ __launch_bounds__(LANES) void lane_search(SearchArgs a) {
         p[T_SKIPPED] = 0;
         p[T_NODES] = t_nodes;
     }
+}
+
+// QSMD_FLAG_EARLY_EXIT_BATCH: histories after the first non-linearisable
+// (or raising) one are SKIPPED, whatever a search kernel wrote for them, and
+// the totals are recounted from the final status / nodes arrays.
+__global__ __launch_bounds__(64) void early_exit_fixup_kernel(uint8_t* status, uint64_t* nodes, uint64_t n,
+                                                             const uint32_t* first_fail,
+                                                             unsigned long long* partials) {
+    const uint32_t ff = *first_fail;
+    uint64_t c[T_N] = {};
+    for (uint64_t h = (uint64_t)blockIdx.x * 64 + threadIdx.x; h < n; h += (uint64_t)gridDim.x * 64) {
+        if (h > ff) {
+            status[h] = QSMD_STATUS_SKIPPED;
+            nodes[h] = 0;
+            c[T_SKIPPED] += 1;
+            continue;
+        }
+        const uint32_t st = status[h];
+        c[T_LIN] += st == QSMD_STATUS_LINEARISABLE;
+        c[T_NONLIN] += st == QSMD_STATUS_NONLINEARISABLE;
+        c[T_ERR] += st == QSMD_STATUS_MODEL_ERROR;
+        c[T_ENC] += st == QSMD_STATUS_ENCODE_ERROR;
+        c[T_BUDGET] += st == QSMD_STATUS_BUDGET;
+        c[T_NODES] += nodes[h];
+    }
+    c[T_CHECKED] = c[T_LIN] + c[T_NONLIN] + c[T_ERR];
+#pragma unroll
+    for (int k = 0; k < T_N; ++k) {
+        const uint64_t s = wave_sum<64>(c[k]);
+        if (threadIdx.x == 0) partials[(uint64_t)blockIdx.x * T_N + k] = s;
+    }
+}
+
+hipError_t launch_early_exit_fixup(uint8_t* status, uint64_t* nodes, uint64_t n, const uint32_t* first_fail,
+                                   unsigned long long* partials, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(early_exit_fixup_kernel, dim3(grid), dim3(64), 0, s, status, nodes, n, first_fail, partials);
+    return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void reduce_totals_kernel(const unsigned long long* partials,

@@ -160,6 +160,32 @@ def test_budget(ctx):
         assert (nd <= budget).all()
 
 
+@pytest.mark.parametrize("name,shift", [("bank_4x16_bugs", 0), ("bank_4x16_bugs", 3000),
+                                        ("bank_6x24", 0), ("bank_4x16", 0)])
+def test_early_exit_batch(ctx, name, shift):
+    """QSMD_FLAG_EARLY_EXIT_BATCH: like QuickCheck stopping at the first
+    failing test, everything after the first non-linearisable (or raising)
+    history is SKIPPED; everything up to it is exactly the full result."""
+    from qsmd import device
+    hdr, ev, _ = gen.generate_config(name, shift, 8000)
+    mid = gen.CONFIGS[name]["model_id"]
+    if name == "bank_6x24":                      # plant one failure deep in the batch
+        ev = ev.copy()
+        k = int(hdr[5000]["ev_off"]) + 47
+        ev["val"][k] += 1 if ev["code"][k] == 7 else 0
+        ev["code"][k] = 7 if ev["code"][k] != 7 else 7
+    st_o, nd_o, _ = oracle_c.check_batch(mid, hdr, ev, threads=8, max_nodes=10**7)
+    fails = np.nonzero((st_o == 0) | (st_o == 2))[0]
+    cut = int(fails[0]) if len(fails) else len(hdr)
+    st, nd, _, tot = ctx.check_arrays(mid, hdr, ev, flags=device.QSMD_FLAG_EXHAUSTIVE |
+                                      device.QSMD_FLAG_EARLY_EXIT_BATCH, max_nodes=10**7)
+    assert np.array_equal(st[:cut + 1], st_o[:cut + 1]) and np.array_equal(nd[:cut + 1], nd_o[:cut + 1])
+    assert (st[cut + 1:] == codec.STATUS_SKIPPED).all() and (nd[cut + 1:] == 0).all()
+    assert tot["skipped"] == max(0, len(hdr) - cut - 1)
+    assert tot["nodes"] == int(nd_o[:cut + 1].sum())
+    assert tot["checked"] == int(((st_o[:cut + 1] <= 2)).sum())
+
+
 def test_encode_errors(ctx):
     hdr = np.zeros(5, dtype=codec.HDR_DTYPE)
     ev = np.zeros(8, dtype=codec.EV_DTYPE)
