@@ -194,7 +194,7 @@ int qsmd_set_time_limit_ms(qsmd_ctx* ctx, uint64_t ms);
  * Default 65536.  Does not change any result. */
 int qsmd_set_stage0_grid(qsmd_ctx* ctx, uint64_t max_blocks);
 
-/* Tuning knob: node budget of the first search stage (default 64).  A history
+/* Tuning knob: node budget of the first search stage (default 0 = none).  A history
  * whose search needs more nodes is searched again, from scratch, by a
  * persistent stage whose idle lanes pull further histories, so one long
  * search does not hold 63 idle lanes.  0 disables.  Results are unchanged. */

@@ -38,7 +38,7 @@ struct qsmd_ctx {
     uint64_t time_limit_ms = 120000;   // safety net per search launch
     uint64_t stage0_max_grid = 65536;  // tuning: cap on stage-0 workgroups (grid-stride beyond)
     unsigned long long* stamps = nullptr;   // diagnostic: stage-0 phase timings
-    uint64_t stage0_budget = 64;       // stage-0 node budget before the refill stage (0 = none)
+    uint64_t stage0_budget = 0;        // stage-0 node budget before the refill stage (0 = none)
 };
 
 namespace {
@@ -193,7 +193,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
 
     // ---- workspace: defer lists, counters, partials, internal totals
     const uint64_t g0 = std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), c->stage0_max_grid);
-    const uint64_t g0b = kRefillGrid;
+    const uint64_t g0b = c->stage0_budget ? kRefillGrid : 0;   // no refill stage without a budget
     const uint64_t gfx = early ? std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), 4096) : 0;
     const uint64_t n_part = g0 + g0b + kStage1Grid + kStage2Grid + gfx;
     // counters: [0] stage-1 list, [1] stage-2 list, [2] timed out, [3] unused,
@@ -255,7 +255,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     ab.list_count = cnt + 4;
     ab.queue_head = cnt + 5;
     ab.partials = part + g0 * T_N;
-    HIP_TRY(c, launch_refill(ab, (uint32_t)g0b, s), "stage 0b launch");
+    if (g0b) HIP_TRY(c, launch_refill(ab, (uint32_t)g0b, s), "stage 0b launch");
     // stage 1: histories with 33..64 events
     SearchArgs a1 = a;
     a1.list = l0;

@@ -128,9 +128,16 @@ def test_mixed_sizes_one_batch(ctx):
 
 @pytest.mark.parametrize("name,n", [("ticket_2x10", 20000), ("bank_4x16", 50000),
                                     ("bank_4x16_bugs", 50000), ("bank_6x24", 20000)])
-def test_generated_configs(ctx, name, n):
-    hdr, ev, bug = gen.generate_config(name, 0, n)
-    st, nd, _ = _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+@pytest.mark.parametrize("budget", [0, 24])
+def test_generated_configs(ctx, name, n, budget):
+    """budget > 0: histories over the stage-0 node budget are searched again by
+    the persistent refill stage (csrc/compact.hip refill_search)."""
+    ctx.set_stage0_budget(budget)
+    try:
+        hdr, ev, bug = gen.generate_config(name, 0, n)
+        st, nd, _ = _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+    finally:
+        ctx.set_stage0_budget(0)
     if name in ("bank_4x16", "bank_6x24"):
         assert (st == codec.STATUS_LIN).all()
 
@@ -153,11 +160,17 @@ def test_model0(ctx):
 
 def test_budget(ctx):
     rng = random.Random(5)
-    hs = [histgen.random_history(rng, "ticket", 40, 1) for _ in range(500)]
-    b = codec.encode(models.TICKET, hs)
-    for budget in (1, 7, 100):
-        st, nd, _ = _compare(ctx, models.MODEL_TICKET, b.hdr, b.events, max_nodes=budget)
-        assert (nd <= budget).all()
+    for n_ev in (40, 24):
+        hs = [histgen.random_history(rng, "ticket", n_ev, 1) for _ in range(500)]
+        b = codec.encode(models.TICKET, hs)
+        for stage0 in (0, 5, 50):
+            ctx.set_stage0_budget(stage0)
+            try:
+                for budget in (1, 7, 100):
+                    st, nd, _ = _compare(ctx, models.MODEL_TICKET, b.hdr, b.events, max_nodes=budget)
+                    assert (nd <= budget).all()
+            finally:
+                ctx.set_stage0_budget(0)
 
 
 @pytest.mark.parametrize("name,shift", [("bank_4x16_bugs", 0), ("bank_4x16_bugs", 3000),
@@ -177,8 +190,12 @@ def test_early_exit_batch(ctx, name, shift):
     st_o, nd_o, _ = oracle_c.check_batch(mid, hdr, ev, threads=8, max_nodes=10**7)
     fails = np.nonzero((st_o == 0) | (st_o == 2))[0]
     cut = int(fails[0]) if len(fails) else len(hdr)
-    st, nd, _, tot = ctx.check_arrays(mid, hdr, ev, flags=device.QSMD_FLAG_EXHAUSTIVE |
-                                      device.QSMD_FLAG_EARLY_EXIT_BATCH, max_nodes=10**7)
+    ctx.set_stage0_budget(32 if shift else 0)
+    try:
+        st, nd, _, tot = ctx.check_arrays(mid, hdr, ev, flags=device.QSMD_FLAG_EXHAUSTIVE |
+                                          device.QSMD_FLAG_EARLY_EXIT_BATCH, max_nodes=10**7)
+    finally:
+        ctx.set_stage0_budget(0)
     assert np.array_equal(st[:cut + 1], st_o[:cut + 1]) and np.array_equal(nd[:cut + 1], nd_o[:cut + 1])
     assert (st[cut + 1:] == codec.STATUS_SKIPPED).all() and (nd[cut + 1:] == 0).all()
     assert tot["skipped"] == max(0, len(hdr) - cut - 1)
