@@ -200,6 +200,82 @@ int qsmd_set_stage0_grid(qsmd_ctx* ctx, uint64_t max_blocks);
  * search does not hold 63 idle lanes.  0 disables.  Results are unchanged. */
 int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
 
+/* Tuning knob: node budget of the per-lane searches (default 4096).  A
+ * history whose search needs more nodes is handed to the split stage, which
+ * searches it again with many lanes (see "Split search" below).  0 disables
+ * the split stage.  Results are unchanged. */
+int qsmd_set_split_budget(qsmd_ctx* ctx, uint64_t nodes);
+
+/* QSMD_FLAG_MEMO: the split stage keeps a table in HBM of search states
+ * (remaining events, model) known to fail, shared by every lane searching the
+ * same history, and prunes a subtree whose root state is in it.  Verdicts
+ * and witnesses are unchanged; node counts become "nodes explored" (fewer
+ * than the reference's, and not reproducible from run to run).  Capacity in
+ * entries of 64 B, a power of two (default 1 << 22 = 256 MiB, allocated on
+ * first use). */
+int qsmd_set_memo_capacity(qsmd_ctx* ctx, uint64_t entries);
+
+/* ----------------------------------------------------------- split search
+ *
+ * One very large history searched by many GPUs.  The
+ * reference DFS (src/Linearisability.hs:52-69) is cut at depth `depth`:
+ * every node it reaches at that depth (a passed postcondition, i.e. a `step`
+ * that recurses) roots a task, its subtree.  Tasks come in the reference's
+ * DFS order, each with the number of nodes the reference counts up to and
+ * including its root.  Searching the tasks anywhere, in any order, and
+ * folding the results in task order (qsmd_combine_tasks) gives the verdict,
+ * exhaustive node count and witness of the single search. */
+#define QSMD_SPLIT_MAX_DEPTH 16
+
+typedef struct qsmd_task {
+    uint32_t hist;          /* history index in the batch (0 for this API)   */
+    uint16_t depth;         /* prefix length d (<= QSMD_SPLIT_MAX_DEPTH)     */
+    uint16_t reserved;
+    uint64_t top_before;    /* reference nodes up to and including the root  */
+    uint8_t  path[QSMD_SPLIT_MAX_DEPTH];  /* invocation event chosen at each */
+                                          /* prefix level (witness indices)  */
+} qsmd_task;
+
+typedef struct qsmd_frontier {
+    uint32_t status;        /* the search above the cut: NONLINEARISABLE =   */
+                            /* exhausted (the tasks decide); LINEARISABLE /  */
+                            /* MODEL_ERROR = decided after top_nodes unless  */
+                            /* a task decides first; BUDGET; ENCODE_ERROR    */
+    uint32_t depth;         /* cut depth chosen                              */
+    uint64_t top_nodes;     /* nodes counted above the cut                   */
+    uint64_t n_tasks;
+} qsmd_frontier;
+
+/* Cut the search of ONE history (hdr[0]) at the smallest depth that yields
+ * at least min_tasks tasks (at most max_tasks, depth <= 16).  witness_out
+ * (n_ev bytes, may be NULL) receives the path when the search above the cut
+ * ends LINEARISABLE. */
+int qsmd_split_frontier(qsmd_ctx* ctx, uint32_t model_id, const qsmd_hdr* hdr,
+                        const qsmd_event* events, uint64_t n_events,
+                        const void* model0, uint32_t flags, uint64_t max_nodes,
+                        uint32_t min_tasks, qsmd_task* tasks_out, uint64_t max_tasks,
+                        qsmd_frontier* frontier_out, uint8_t* witness_out);
+
+/* Search the subtrees of tasks[0..n_tasks) of history hdr[0] (tasks in DFS
+ * order; any subset of a frontier, kept in order).  Per task: status
+ * LINEARISABLE = the subtree holds a linearisation, NONLINEARISABLE = it
+ * does not, MODEL_ERROR, BUDGET, SKIPPED = not searched because an earlier
+ * task of this call decided; nodes = nodes of the subtree below its root
+ * up to its decision; witness_out (n_tasks x 64 B, may be NULL) = the full
+ * path of a LINEARISABLE task.  QSMD_FLAG_MEMO applies. */
+int qsmd_check_tasks(qsmd_ctx* ctx, uint32_t model_id, const qsmd_hdr* hdr,
+                     const qsmd_event* events, uint64_t n_events,
+                     const void* model0, uint32_t flags, uint64_t max_nodes,
+                     const qsmd_task* tasks, uint64_t n_tasks,
+                     uint8_t* status_out, uint64_t* nodes_out, uint8_t* witness_out);
+
+/* Fold task results in DFS order (host only, no device).  winner_out = index
+ * of the deciding task, -1 when the decision came from above the cut. */
+int qsmd_combine_tasks(const qsmd_frontier* frontier, const qsmd_task* tasks,
+                       const uint8_t* status, const uint64_t* nodes, uint64_t n_tasks,
+                       uint64_t max_nodes, uint8_t* status_out, uint64_t* nodes_out,
+                       int64_t* winner_out);
+
 /* Diagnostic: when stamps_dev (device memory, 4 x u64 per stage-0
  * workgroup) is non-NULL, stage 0 runs an instrumented build that records
  * per-workgroup s_memtime totals of its phases (staging, search, output,

@@ -33,14 +33,17 @@ def lib():
             ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_void_p, ctypes.c_int]
+        L.oracle_check_batch_flags.restype = ctypes.c_int
+        L.oracle_check_batch_flags.argtypes = L.oracle_check_batch.argtypes + [ctypes.c_uint32]
         _lib = L
     return _lib
 
 
-def check_batch(model_id, hdr, events, model0=None, max_nodes=0, threads=1, witness=False):
+def check_batch(model_id, hdr, events, model0=None, max_nodes=0, threads=1, witness=False, memo=False):
     """Run the oracle.  hdr/events are numpy arrays in the include/qsmd.h
-    layout; model0 is None or a ctypes struct.  Returns (status, nodes,
-    witness_or_None)."""
+    layout; model0 is None or a ctypes struct.  memo=True prunes known-failing
+    states (verdicts exact, node counts not the reference's).  Returns
+    (status, nodes, witness_or_None)."""
     n = len(hdr)
     hdr = np.ascontiguousarray(hdr)
     events = np.ascontiguousarray(events)
@@ -48,8 +51,8 @@ def check_batch(model_id, hdr, events, model0=None, max_nodes=0, threads=1, witn
     nodes = np.zeros(n, dtype=np.uint64)
     wit = np.full(max(len(events), 1), 0xFF, dtype=np.uint8) if witness else None
     m0 = ctypes.cast(ctypes.pointer(model0), ctypes.c_void_p) if model0 is not None else None
-    lib().oracle_check_batch(
+    lib().oracle_check_batch_flags(
         model_id, hdr.ctypes.data, n, events.ctypes.data if len(events) else None,
         m0, max_nodes, status.ctypes.data, nodes.ctypes.data,
-        wit.ctypes.data if wit is not None else None, threads)
+        wit.ctypes.data if wit is not None else None, threads, 2 if memo else 0)
     return status, nodes, wit

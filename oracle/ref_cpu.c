@@ -68,7 +68,65 @@ typedef struct {
     uint64_t nodes, max_nodes;
     uint8_t path[QSMD_MAX_EVENTS];
     int depth;
+    struct memo_t* memo;                 /* QSMD_FLAG_MEMO: failed states, or NULL */
 } search_t;
+
+/* ------------------------------------------------------------- memo */
+/* QSMD_FLAG_MEMO restated: a state (counter vector k, model) whose subtree
+ * was searched completely without success is remembered; reaching it again
+ * counts the node (its postcondition was evaluated) and skips the subtree.
+ * The outcome of a subtree is a function of the state alone (Lemma L1), so
+ * verdicts are those of the exhaustive search. */
+#define MEMO_KEY (QSMD_MAX_PIDS + 1 + 8 * 9)
+typedef struct memo_t {
+    uint8_t* keys;     /* cap x MEMO_KEY */
+    uint8_t* used;
+    uint64_t cap, n;
+} memo_t;
+
+static uint64_t memo_hash(const uint8_t* k) {
+    uint64_t h = 1469598103934665603ull;
+    for (int i = 0; i < MEMO_KEY; ++i) { h ^= k[i]; h *= 1099511628211ull; }
+    return h;
+}
+
+static void memo_key(const search_t* s, const model_u* m, uint8_t* k) {
+    memset(k, 0, MEMO_KEY);
+    memcpy(k, s->k, (size_t)s->n_pid);
+    uint8_t* q = k + QSMD_MAX_PIDS;
+    if (s->model_id == QSMD_MODEL_BANK) {
+        q[0] = (uint8_t)m->bank.exists;
+        for (int a = 0; a < QSMD_BANK_MAX_ACCOUNTS; ++a) memcpy(q + 1 + 8 * a, &m->bank.bal[a], 8);
+    } else {
+        q[0] = (uint8_t)m->ticket.is_just;
+        memcpy(q + 1, &m->ticket.n, 8);
+    }
+}
+
+static int memo_find(memo_t* t, const uint8_t* k, int insert) {
+    if (insert && 2 * (t->n + 1) > t->cap) {             /* grow: rehash */
+        memo_t u = {0};
+        u.cap = t->cap ? 2 * t->cap : 1024;
+        u.keys = (uint8_t*)malloc(u.cap * MEMO_KEY);
+        u.used = (uint8_t*)calloc(u.cap, 1);
+        for (uint64_t i = 0; i < t->cap; ++i)
+            if (t->used[i]) memo_find(&u, t->keys + i * MEMO_KEY, 1);
+        free(t->keys);
+        free(t->used);
+        *t = u;
+    }
+    if (!t->cap) return 0;
+    for (uint64_t i = memo_hash(k) & (t->cap - 1);; i = (i + 1) & (t->cap - 1)) {
+        if (!t->used[i]) {
+            if (!insert) return 0;
+            memcpy(t->keys + i * MEMO_KEY, k, MEMO_KEY);
+            t->used[i] = 1;
+            t->n++;
+            return 1;
+        }
+        if (memcmp(t->keys + i * MEMO_KEY, k, MEMO_KEY) == 0) return 1;
+    }
+}
 
 /* ------------------------------------------------------------- models */
 
@@ -209,7 +267,15 @@ static int step(search_t* s, const model_u* m, int p, int e, int r) {
     next_of(s, &m2, &s->ev[e]);
     s->path[s->depth++] = (uint8_t)e;
     s->k[p]++;
-    int res = expand(s, &m2, 0);
+    int res;
+    uint8_t key[MEMO_KEY];
+    if (s->memo) memo_key(s, &m2, key);
+    if (s->memo && memo_find(s->memo, key, 0)) {
+        res = R_FALSE;                               /* known to fail */
+    } else {
+        res = expand(s, &m2, 0);
+        if (s->memo && res == R_FALSE) memo_find(s->memo, key, 1);
+    }
     s->k[p]--;
     if (res != R_TRUE) s->depth--;
     return res;
@@ -254,9 +320,19 @@ static void model_init(uint32_t model_id, const void* model0, model_u* m) {
 }
 
 /* Check one history.  Returns the QSMD_STATUS_* code. */
+static uint8_t check_one(uint32_t model_id, const qsmd_hdr* h, const qsmd_event* events,
+                         const void* model0, uint64_t max_nodes, uint64_t* nodes_out,
+                         uint8_t* witness, memo_t* memo);
+
 uint8_t oracle_check_one(uint32_t model_id, const qsmd_hdr* h, const qsmd_event* events,
                          const void* model0, uint64_t max_nodes,
                          uint64_t* nodes_out, uint8_t* witness /* n_ev bytes or NULL */) {
+    return check_one(model_id, h, events, model0, max_nodes, nodes_out, witness, NULL);
+}
+
+static uint8_t check_one(uint32_t model_id, const qsmd_hdr* h, const qsmd_event* events,
+                         const void* model0, uint64_t max_nodes, uint64_t* nodes_out,
+                         uint8_t* witness, memo_t* memo) {
     const qsmd_event* ev = events + h->ev_off;
     *nodes_out = 0;
     if (!valid_history(model_id, h, ev)) return QSMD_STATUS_ENCODE_ERROR;
@@ -271,6 +347,7 @@ uint8_t oracle_check_one(uint32_t model_id, const qsmd_hdr* h, const qsmd_event*
     s.nodes = 0;
     s.max_nodes = max_nodes;
     s.depth = 0;
+    s.memo = memo;
     uint8_t ninv[QSMD_MAX_PIDS];
     memset(ninv, 0, sizeof(ninv));
     memset(s.nresp, 0, sizeof(s.nresp));
@@ -318,6 +395,7 @@ typedef struct {
     uint64_t* nodes;
     uint8_t* witness;
     uint64_t lo, hi;
+    int memo;
 } job_t;
 
 static void* run_job(void* arg) {
@@ -325,8 +403,11 @@ static void* run_job(void* arg) {
     for (uint64_t i = j->lo; i < j->hi; ++i) {
         uint64_t n = 0;
         uint8_t* w = j->witness ? j->witness + j->hdr[i].ev_off : NULL;
-        j->status[i] = oracle_check_one(j->model_id, &j->hdr[i], j->events, j->model0,
-                                        j->max_nodes, &n, w);
+        memo_t m = {0};
+        j->status[i] = check_one(j->model_id, &j->hdr[i], j->events, j->model0,
+                                 j->max_nodes, &n, w, j->memo ? &m : NULL);
+        free(m.keys);
+        free(m.used);
         if (j->nodes) j->nodes[i] = n;
     }
     return NULL;
@@ -334,9 +415,23 @@ static void* run_job(void* arg) {
 
 /* Check histories [0, n_hist) with n_threads host threads (history shards).
  * Witness (nullable) is indexed like the events array. Returns 0. */
+int oracle_check_batch_flags(uint32_t model_id, const qsmd_hdr* hdr, uint64_t n_hist,
+                             const qsmd_event* events, const void* model0, uint64_t max_nodes,
+                             uint8_t* status, uint64_t* nodes, uint8_t* witness, int n_threads,
+                             uint32_t flags);
+
 int oracle_check_batch(uint32_t model_id, const qsmd_hdr* hdr, uint64_t n_hist,
                        const qsmd_event* events, const void* model0, uint64_t max_nodes,
                        uint8_t* status, uint64_t* nodes, uint8_t* witness, int n_threads) {
+    return oracle_check_batch_flags(model_id, hdr, n_hist, events, model0, max_nodes, status, nodes,
+                                    witness, n_threads, 0);
+}
+
+/* flags: QSMD_FLAG_MEMO prunes known-failing states (verdicts only). */
+int oracle_check_batch_flags(uint32_t model_id, const qsmd_hdr* hdr, uint64_t n_hist,
+                             const qsmd_event* events, const void* model0, uint64_t max_nodes,
+                             uint8_t* status, uint64_t* nodes, uint8_t* witness, int n_threads,
+                             uint32_t flags) {
     if (n_threads < 1) n_threads = 1;
     if ((uint64_t)n_threads > n_hist) n_threads = n_hist ? (int)n_hist : 1;
     job_t jobs[256];
@@ -345,7 +440,8 @@ int oracle_check_batch(uint32_t model_id, const qsmd_hdr* hdr, uint64_t n_hist,
     uint64_t per = (n_hist + n_threads - 1) / n_threads;
     for (int t = 0; t < n_threads; ++t) {
         jobs[t] = (job_t){model_id, hdr, events, model0, max_nodes, status, nodes, witness,
-                          t * per, (t + 1) * per > n_hist ? n_hist : (t + 1) * per};
+                          t * per, (t + 1) * per > n_hist ? n_hist : (t + 1) * per,
+                          (flags & QSMD_FLAG_MEMO) != 0};
         if (jobs[t].lo > jobs[t].hi) jobs[t].lo = jobs[t].hi;
     }
     if (n_threads == 1) { run_job(&jobs[0]); return 0; }

@@ -39,6 +39,14 @@ struct qsmd_ctx {
     uint64_t stage0_max_grid = 65536;  // tuning: cap on stage-0 workgroups (grid-stride beyond)
     unsigned long long* stamps = nullptr;   // diagnostic: stage-0 phase timings
     uint64_t stage0_budget = 0;        // stage-0 node budget before the refill stage (0 = none)
+    uint64_t split_budget = 4096;      // per-lane node budget before the split stage (0 = none)
+    // QSMD_FLAG_MEMO table (device), allocated on first use
+    unsigned long long* memo = nullptr;
+    uint64_t memo_entries = 1ull << 22;
+    uint64_t memo_alloc = 0;
+    // split-search entry points: their own device buffers
+    char* sx = nullptr;
+    size_t sx_bytes = 0;
 };
 
 namespace {
@@ -47,6 +55,12 @@ constexpr uint32_t kStage1Grid = 1024;   // list-mode stages: grid-stride
 constexpr uint32_t kStage2Grid = 1024;
 constexpr uint32_t kRefillGrid = 2048;   // persistent: 8 wavefronts per CU
 constexpr uint64_t kTimingSlots = 1024;
+constexpr uint32_t kFrontierGrid = 256;  // split stage: one lane per giant history, grid-stride
+constexpr uint32_t kTaskGrid[SPLIT_VARIANTS] = {1024, 512};   // persistent task wavefronts
+constexpr uint32_t kCombineGrid = 64;
+constexpr uint32_t kTaskCap = 1u << 19;  // tasks per variant per call (beyond: searched unsplit)
+constexpr uint32_t kSplitTarget = 256;   // tasks wanted per giant history
+constexpr uint32_t kSplitMaxTasks = 4096;
 
 int fail(qsmd_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
     if (c) {
@@ -146,6 +160,8 @@ void qsmd_close(qsmd_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->ws) (void)hipFree(c->ws);
+    if (c->sx) (void)hipFree(c->sx);
+    if (c->memo) (void)hipFree(c->memo);
     if (c->io) (void)hipFree(c->io);
     for (auto e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -165,6 +181,18 @@ int qsmd_set_stage0_budget(qsmd_ctx* c, uint64_t nodes) {
     return QSMD_OK;
 }
 
+int qsmd_set_split_budget(qsmd_ctx* c, uint64_t nodes) {
+    if (!c) return QSMD_ERR_ARG;
+    c->split_budget = nodes;
+    return QSMD_OK;
+}
+
+int qsmd_set_memo_capacity(qsmd_ctx* c, uint64_t entries) {
+    if (!c || entries < 1024 || (entries & (entries - 1)) || entries > (1ull << 32)) return QSMD_ERR_ARG;
+    c->memo_entries = entries;
+    return QSMD_OK;
+}
+
 int qsmd_set_stage0_grid(qsmd_ctx* c, uint64_t max_blocks) {
     if (!c || max_blocks == 0 || max_blocks > 0x7FFFFFFFull) return QSMD_ERR_ARG;
     c->stage0_max_grid = max_blocks;
@@ -174,6 +202,24 @@ int qsmd_set_stage0_grid(qsmd_ctx* c, uint64_t max_blocks) {
 int qsmd_set_time_limit_ms(qsmd_ctx* c, uint64_t ms) {
     if (!c) return QSMD_ERR_ARG;
     c->time_limit_ms = ms;
+    return QSMD_OK;
+}
+
+// The memo table, cleared for this call (entries are only valid within one).
+static int memo_prepare(qsmd_ctx* c, hipStream_t s, unsigned long long** out) {
+    if (c->memo_alloc != c->memo_entries) {
+        if (c->memo) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(c->memo);
+            c->memo = nullptr;
+            c->memo_alloc = 0;
+        }
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->memo), c->memo_entries * 64);
+        if (e != hipSuccess) return fail(c, QSMD_ERR_NOMEM, "hipMalloc memo table", e);
+        c->memo_alloc = c->memo_entries;
+    }
+    HIP_TRY(c, hipMemsetAsync(c->memo, 0, c->memo_alloc * 64, s), "memset memo table");
+    *out = c->memo;
     return QSMD_OK;
 }
 
@@ -195,16 +241,27 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const uint64_t g0 = std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), c->stage0_max_grid);
     const uint64_t g0b = c->stage0_budget ? kRefillGrid : 0;   // no refill stage without a budget
     const uint64_t gfx = early ? std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), 4096) : 0;
-    const uint64_t n_part = g0 + g0b + kStage1Grid + kStage2Grid + gfx;
+    const bool split = c->split_budget && (!max_nodes || c->split_budget < max_nodes);
+    const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
+    const uint64_t gsp = split ? kCombineGrid : 0;
+    const uint64_t n_part = g0 + g0b + kStage1Grid + kStage2Grid + gsp + gfx;
     // counters: [0] stage-1 list, [1] stage-2 list, [2] timed out, [3] unused,
-    //           [4] heavy list, [5] heavy queue head, [6] first failing history
+    //           [4] heavy list, [5] heavy queue head, [6] first failing history,
+    //           [7] giant list, [8..9] tasks per variant, [10..11] task queue heads
     const size_t off_cnt = 0;
     const size_t off_tot = 256;                                        // qsmd_totals
     const size_t off_l0 = 512;
     const size_t off_l1 = off_l0 + align_up(n_hist * 4 + 4);
     const size_t off_lh = off_l1 + align_up(n_hist * 4 + 4);
-    const size_t off_nd = off_lh + align_up(n_hist * 4 + 4);          // nodes if the caller has none
-    const size_t off_part = off_nd + (early && !nodes ? align_up(n_hist * 8) : 0);
+    const size_t off_lg = off_lh + align_up(n_hist * 4 + 4);
+    const size_t off_nd = off_lg + (split ? align_up(n_hist * 4 + 4) : 0);   // nodes if the caller has none
+    const size_t off_gr = off_nd + (early && !nodes ? align_up(n_hist * 8) : 0);
+    const size_t off_tk = off_gr + (split ? align_up(n_hist * sizeof(GiantRec)) : 0);
+    const uint64_t n_tk = split ? (uint64_t)SPLIT_VARIANTS * kTaskCap : 0;
+    const size_t off_ts = off_tk + align_up(n_tk * sizeof(qsmd_task));
+    const size_t off_tn = off_ts + align_up(n_tk);
+    const size_t off_tw = off_tn + align_up(n_tk * 8);
+    const size_t off_part = off_tw + (want_w ? align_up(n_tk * kTaskWitness) : 0);
     const size_t need = off_part + align_up(n_part * T_N * 8);
     rc = grow(c, &c->ws, &c->ws_bytes, need);
     if (rc) return rc;
@@ -216,7 +273,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     unsigned long long* part = reinterpret_cast<unsigned long long*>(c->ws + off_part);
     if (early && !nodes) nodes = reinterpret_cast<uint64_t*>(c->ws + off_nd);
 
-    HIP_TRY(c, hipMemsetAsync(cnt, 0, 32, s), "memset counters");
+    HIP_TRY(c, hipMemsetAsync(cnt, 0, 64, s), "memset counters");
     HIP_TRY(c, hipMemsetAsync(cnt + 6, 0xFF, 4, s), "memset first_fail");
     HIP_TRY(c, hipMemsetAsync(tot, 0, sizeof(qsmd_totals), s), "memset totals");
     a.first_fail = early ? cnt + 6 : nullptr;
@@ -233,6 +290,12 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a.nodes = nodes;
     a.witness = (flags & QSMD_FLAG_WITNESS) ? witness : nullptr;
     a.timed_out = cnt + 2;
+    uint32_t* lg = reinterpret_cast<uint32_t*>(c->ws + off_lg);
+    if (split) {
+        a.giant_list = lg;
+        a.giant_count = cnt + 7;
+        a.split_budget = c->split_budget;
+    }
 
     hipEvent_t* evs = &c->ev[3 * (c->n_calls % kTimingSlots)];
     HIP_TRY(c, hipEventRecord(evs[0], s), "hipEventRecord");
@@ -244,9 +307,15 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.defer_count = cnt + 0;
     a0.partials = part;
     a0.stamps = c->stamps;
-    a0.heavy_list = c->stage0_budget ? lh : nullptr;
-    a0.heavy_count = cnt + 4;
-    a0.stage0_budget = c->stage0_budget;
+    if (c->stage0_budget) {             // stage 0 -> refill -> (split)
+        a0.heavy_list = lh;
+        a0.heavy_count = cnt + 4;
+        a0.stage0_budget = c->stage0_budget;
+    } else if (split) {                 // stage 0 -> split
+        a0.heavy_list = lg;
+        a0.heavy_count = cnt + 7;
+        a0.stage0_budget = c->split_budget;
+    }
     HIP_TRY(c, launch_compact(a0, (uint32_t)g0, s), "stage 0 launch");
     HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
     // stage 0b: histories over the stage-0 node budget, persistent refill
@@ -272,8 +341,36 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a2.defer_count = cnt + 3;
     a2.partials = part + (g0 + g0b + kStage1Grid) * T_N;
     HIP_TRY(c, launch_stage(2, a2, kStage2Grid, s), "stage 2 launch");
+    if (split) {
+        SplitArgs p{};
+        p.s = a;
+        p.s.partials = part + (g0 + g0b + kStage1Grid + kStage2Grid) * T_N;
+        p.giant_list = lg;
+        p.giant_count = cnt + 7;
+        p.giants = reinterpret_cast<GiantRec*>(c->ws + off_gr);
+        p.tasks = reinterpret_cast<qsmd_task*>(c->ws + off_tk);
+        p.task_count = cnt + 8;
+        p.queue_head = cnt + 10;
+        p.task_cap = kTaskCap;
+        p.target = kSplitTarget;
+        p.max_tasks = kSplitMaxTasks;
+        p.max_depth = QSMD_SPLIT_MAX_DEPTH;
+        p.task_status = reinterpret_cast<uint8_t*>(c->ws + off_ts);
+        p.task_nodes = reinterpret_cast<uint64_t*>(c->ws + off_tn);
+        p.task_witness = want_w ? reinterpret_cast<uint8_t*>(c->ws + off_tw) : nullptr;
+        if (flags & QSMD_FLAG_MEMO) {
+            rc = memo_prepare(c, s, &p.memo);
+            if (rc) return rc;
+            p.memo_mask = c->memo_alloc - 1;
+        }
+        for (int v = 0; v < SPLIT_VARIANTS; ++v)
+            HIP_TRY(c, launch_frontier(v, p, kFrontierGrid, s), "frontier launch");
+        for (int v = 0; v < SPLIT_VARIANTS; ++v)
+            HIP_TRY(c, launch_tasks(v, p, kTaskGrid[v], s), "task launch");
+        HIP_TRY(c, launch_combine(p, kCombineGrid, s), "combine launch");
+    }
     if (early) {
-        unsigned long long* pf = part + (g0 + g0b + kStage1Grid + kStage2Grid) * T_N;
+        unsigned long long* pf = part + (g0 + g0b + kStage1Grid + kStage2Grid + gsp) * T_N;
         HIP_TRY(c, launch_early_exit_fixup(status, nodes, n_hist, cnt + 6, pf, (uint32_t)gfx, s), "fixup launch");
         HIP_TRY(c, launch_reduce(pf, gfx, tot, s), "reduce launch");
     } else {
@@ -366,6 +463,186 @@ int qsmd_timing_read(qsmd_ctx* c, float* stage0_ms, float* call_ms, uint64_t max
         if (call_ms) HIP_TRY(c, hipEventElapsedTime(&call_ms[i], evs[0], evs[2]), "elapsed");
     }
     *n_out = n;
+    return QSMD_OK;
+}
+
+// ------------------------------------------------------------ split search
+
+static bool split_hdr_ok(const qsmd_hdr* h, uint64_t n_events) {
+    return h->n_ev <= QSMD_MAX_EVENTS && h->n_pid <= QSMD_MAX_PIDS && (uint64_t)h->ev_off + h->n_ev <= n_events;
+}
+
+static uint32_t split_variant(const qsmd_hdr* h) { return (h->n_ev <= 64 && h->n_pid <= 8) ? 0u : 1u; }
+
+int qsmd_split_frontier(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, const qsmd_event* events,
+                        uint64_t n_events, const void* model0, uint32_t flags, uint64_t max_nodes,
+                        uint32_t min_tasks, qsmd_task* tasks_out, uint64_t max_tasks, qsmd_frontier* fr,
+                        uint8_t* witness_out) {
+    if (!c) return QSMD_ERR_ARG;
+    if (!hdr || !fr || (max_tasks && !tasks_out) || (n_events && !events))
+        return fail(c, QSMD_ERR_ARG, "null argument");
+    if (model_id != QSMD_MODEL_BANK && model_id != QSMD_MODEL_TICKET) return fail(c, QSMD_ERR_ARG, "unknown model_id");
+    if (max_tasks > (1ull << 24)) return fail(c, QSMD_ERR_ARG, "max_tasks > 2^24");
+    std::lock_guard<std::mutex> g(c->mu);
+    SearchArgs a{};
+    int rc = fill_model0(c, model_id, model0, a);
+    if (rc) return rc;
+    std::memset(fr, 0, sizeof *fr);
+    if (!split_hdr_ok(hdr, n_events) || hdr->model_id != model_id) {
+        fr->status = QSMD_STATUS_ENCODE_ERROR;
+        return QSMD_OK;
+    }
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    hipStream_t s = c->stream;
+    const uint64_t cap = std::max<uint64_t>(max_tasks, 1);
+    const size_t o_hdr = 0, o_cnt = 256, o_gl = 512, o_gr = 768;
+    const size_t o_ev = 1024;
+    const size_t o_tk = o_ev + align_up(n_events * sizeof(qsmd_event));
+    const size_t o_w = o_tk + align_up(SPLIT_VARIANTS * cap * sizeof(qsmd_task));
+    const size_t need = o_w + align_up(QSMD_MAX_EVENTS);
+    rc = grow(c, &c->sx, &c->sx_bytes, need);
+    if (rc) return rc;
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(c->sx + o_cnt);
+    const uint32_t one = 1;
+    HIP_TRY(c, hipMemcpyAsync(c->sx + o_hdr, hdr, sizeof *hdr, hipMemcpyHostToDevice, s), "H2D hdr");
+    if (n_events)
+        HIP_TRY(c, hipMemcpyAsync(c->sx + o_ev, events, n_events * sizeof(qsmd_event), hipMemcpyHostToDevice, s), "H2D events");
+    HIP_TRY(c, hipMemsetAsync(cnt, 0, 64, s), "memset counters");
+    HIP_TRY(c, hipMemsetAsync(c->sx + o_gl, 0, 4, s), "memset giant list");
+    HIP_TRY(c, hipMemcpyAsync(cnt + 7, &one, 4, hipMemcpyHostToDevice, s), "H2D giant count");
+    a.hdr = reinterpret_cast<const qsmd_hdr*>(c->sx + o_hdr);
+    a.events = reinterpret_cast<const uint2*>(c->sx + o_ev);
+    a.n_hist = 1;
+    a.n_events = n_events;
+    a.flags = flags;
+    a.model_id = model_id;
+    a.max_nodes = max_nodes;
+    a.time_limit = c->time_limit_ms * 100000ull;
+    a.timed_out = cnt + 2;
+    a.witness = witness_out ? reinterpret_cast<uint8_t*>(c->sx + o_w) : nullptr;
+    SplitArgs p{};
+    p.s = a;
+    p.giant_list = reinterpret_cast<const uint32_t*>(c->sx + o_gl);
+    p.giant_count = cnt + 7;
+    p.giants = reinterpret_cast<GiantRec*>(c->sx + o_gr);
+    p.tasks = reinterpret_cast<qsmd_task*>(c->sx + o_tk);
+    p.task_count = cnt + 8;
+    p.queue_head = cnt + 10;
+    p.task_cap = (uint32_t)cap;
+    p.target = std::max<uint32_t>(min_tasks, 1);
+    p.max_tasks = (uint32_t)max_tasks;
+    p.max_depth = QSMD_SPLIT_MAX_DEPTH;
+    for (int v = 0; v < SPLIT_VARIANTS; ++v) HIP_TRY(c, launch_frontier(v, p, 1, s), "frontier launch");
+    GiantRec G{};
+    HIP_TRY(c, hipMemcpyAsync(&G, p.giants, sizeof G, hipMemcpyDeviceToHost, s), "D2H giant");
+    HIP_TRY(c, hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (G.n_tasks)
+        HIP_TRY(c, hipMemcpy(tasks_out, p.tasks + (uint64_t)G.variant * cap + G.first, G.n_tasks * sizeof(qsmd_task),
+                             hipMemcpyDeviceToHost), "D2H tasks");
+    if (witness_out && G.term_status == QSMD_STATUS_LINEARISABLE && hdr->n_ev)
+        HIP_TRY(c, hipMemcpy(witness_out, c->sx + o_w, hdr->n_ev, hipMemcpyDeviceToHost), "D2H witness");
+    fr->status = G.term_status;
+    fr->depth = G.depth;
+    fr->top_nodes = G.term_nodes;
+    fr->n_tasks = G.n_tasks;
+    return QSMD_OK;
+}
+
+int qsmd_check_tasks(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, const qsmd_event* events,
+                     uint64_t n_events, const void* model0, uint32_t flags, uint64_t max_nodes,
+                     const qsmd_task* tasks, uint64_t n_tasks, uint8_t* status_out, uint64_t* nodes_out,
+                     uint8_t* witness_out) {
+    if (!c) return QSMD_ERR_ARG;
+    if (!hdr || (n_tasks && (!tasks || !status_out)) || (n_events && !events))
+        return fail(c, QSMD_ERR_ARG, "null argument");
+    if (model_id != QSMD_MODEL_BANK && model_id != QSMD_MODEL_TICKET) return fail(c, QSMD_ERR_ARG, "unknown model_id");
+    if (n_tasks > (1ull << 24)) return fail(c, QSMD_ERR_ARG, "n_tasks > 2^24");
+    if (hdr->model_id != model_id || !split_hdr_ok(hdr, n_events)) return fail(c, QSMD_ERR_ARG, "bad history header");
+    for (uint64_t i = 0; i < n_tasks; ++i) {
+        if (tasks[i].hist != 0 || tasks[i].depth > QSMD_SPLIT_MAX_DEPTH || 2u * tasks[i].depth > hdr->n_ev)
+            return fail(c, QSMD_ERR_ARG, "bad task (hist must be 0, depth <= 16)");
+        for (uint32_t d = 0; d < tasks[i].depth; ++d)
+            if (tasks[i].path[d] >= hdr->n_ev) return fail(c, QSMD_ERR_ARG, "bad task path");
+    }
+    std::lock_guard<std::mutex> g(c->mu);
+    SearchArgs a{};
+    int rc = fill_model0(c, model_id, model0, a);
+    if (rc) return rc;
+    if (!n_tasks) return QSMD_OK;
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    hipStream_t s = c->stream;
+    const uint32_t v = split_variant(hdr);
+    const uint64_t n = n_tasks;
+    const bool want_w = witness_out != nullptr;
+    const size_t o_hdr = 0, o_cnt = 256, o_gr = 512;
+    const size_t o_ev = 1024;
+    const size_t o_tk = o_ev + align_up(n_events * sizeof(qsmd_event));
+    const size_t o_ts = o_tk + align_up(SPLIT_VARIANTS * n * sizeof(qsmd_task));
+    const size_t o_tn = o_ts + align_up(SPLIT_VARIANTS * n);
+    const size_t o_tw = o_tn + align_up(SPLIT_VARIANTS * n * 8);
+    const size_t need = o_tw + (want_w ? align_up(SPLIT_VARIANTS * n * kTaskWitness) : 0);
+    rc = grow(c, &c->sx, &c->sx_bytes, need);
+    if (rc) return rc;
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(c->sx + o_cnt);
+    GiantRec G{};
+    G.h = 0;
+    G.variant = v;
+    G.first = 0;
+    G.n_tasks = (uint32_t)n;
+    G.term_status = QSMD_STATUS_NONLINEARISABLE;
+    G.min_win = ~0u;
+    uint32_t counts[16] = {};
+    counts[8 + v] = (uint32_t)n;
+    HIP_TRY(c, hipMemcpyAsync(c->sx + o_hdr, hdr, sizeof *hdr, hipMemcpyHostToDevice, s), "H2D hdr");
+    if (n_events)
+        HIP_TRY(c, hipMemcpyAsync(c->sx + o_ev, events, n_events * sizeof(qsmd_event), hipMemcpyHostToDevice, s), "H2D events");
+    HIP_TRY(c, hipMemcpyAsync(cnt, counts, sizeof counts, hipMemcpyHostToDevice, s), "H2D counters");
+    HIP_TRY(c, hipMemcpyAsync(c->sx + o_gr, &G, sizeof G, hipMemcpyHostToDevice, s), "H2D giant");
+    auto* d_tk = reinterpret_cast<qsmd_task*>(c->sx + o_tk);
+    HIP_TRY(c, hipMemcpyAsync(d_tk + v * n, tasks, n * sizeof(qsmd_task), hipMemcpyHostToDevice, s), "H2D tasks");
+    a.hdr = reinterpret_cast<const qsmd_hdr*>(c->sx + o_hdr);
+    a.events = reinterpret_cast<const uint2*>(c->sx + o_ev);
+    a.n_hist = 1;
+    a.n_events = n_events;
+    a.flags = flags;
+    a.model_id = model_id;
+    a.max_nodes = max_nodes;
+    a.time_limit = c->time_limit_ms * 100000ull;
+    a.timed_out = cnt + 2;
+    SplitArgs p{};
+    p.s = a;
+    p.giants = reinterpret_cast<GiantRec*>(c->sx + o_gr);
+    p.tasks = d_tk;
+    p.task_count = cnt + 8;
+    p.queue_head = cnt + 10;
+    p.task_cap = (uint32_t)n;
+    p.task_status = reinterpret_cast<uint8_t*>(c->sx + o_ts);
+    p.task_nodes = reinterpret_cast<uint64_t*>(c->sx + o_tn);
+    p.task_witness = want_w ? reinterpret_cast<uint8_t*>(c->sx + o_tw) : nullptr;
+    p.external_tasks = 1;
+    if (flags & QSMD_FLAG_MEMO) {
+        rc = memo_prepare(c, s, &p.memo);
+        if (rc) return rc;
+        p.memo_mask = c->memo_alloc - 1;
+    }
+    HIP_TRY(c, launch_tasks((int)v, p, kTaskGrid[v], s), "task launch");
+    HIP_TRY(c, hipMemcpyAsync(status_out, p.task_status + v * n, n, hipMemcpyDeviceToHost, s), "D2H status");
+    if (nodes_out)
+        HIP_TRY(c, hipMemcpyAsync(nodes_out, p.task_nodes + v * n, n * 8, hipMemcpyDeviceToHost, s), "D2H nodes");
+    if (want_w)
+        HIP_TRY(c, hipMemcpyAsync(witness_out, p.task_witness + v * n * kTaskWitness, n * kTaskWitness,
+                                  hipMemcpyDeviceToHost, s), "D2H witness");
+    HIP_TRY(c, hipStreamSynchronize(s), "hipStreamSynchronize");
+    return QSMD_OK;
+}
+
+int qsmd_combine_tasks(const qsmd_frontier* fr, const qsmd_task* tasks, const uint8_t* status,
+                       const uint64_t* nodes, uint64_t n_tasks, uint64_t max_nodes, uint8_t* status_out,
+                       uint64_t* nodes_out, int64_t* winner_out) {
+    if (!fr || !status_out || !nodes_out || !winner_out || (n_tasks && (!tasks || !status || !nodes)))
+        return QSMD_ERR_ARG;
+    *status_out = (uint8_t)combine_tasks(fr->status, fr->top_nodes, tasks, status, nodes, n_tasks, max_nodes,
+                                         nodes_out, winner_out);
     return QSMD_OK;
 }
 

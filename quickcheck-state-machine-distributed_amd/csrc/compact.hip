@@ -277,6 +277,7 @@ struct LaneDFS {
     static constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
     uint32_t INV, RESP, P0, P1, P2, ALL;
     uint32_t rem, cand, depth, ex, neg, RS, found;
+    uint32_t base;          // depth of the search root (0; the task depth in split_search)
     uint64_t nodes;
     Stack16 stk;
 
@@ -292,7 +293,7 @@ struct LaneDFS {
         ALL = INV | RESP;
         rem = ALL;
         cand = cands(rem, INV, RESP);
-        depth = 0; found = 0; nodes = 0; RS = 0;
+        depth = 0; found = 0; nodes = 0; RS = 0; base = 0;
         stk.w[0] = stk.w[1] = stk.w[2] = stk.w[3] = 0u;
         ex = a.m0_exists; neg = 0;
         if constexpr (BANK) {
@@ -306,10 +307,15 @@ struct LaneDFS {
         }
     }
 
-    __device__ __forceinline__ int step(const SearchArgs& a, const uint32_t (*s_ev)[C_LANES],
+    // evc[e * STRIDE] = compressed event e (the lane's LDS column: STRIDE = 64;
+    // a history shared by the wavefront: STRIDE = 1)
+    template <int STRIDE>
+    __device__ __forceinline__ int step(const SearchArgs& a, const uint32_t* evc,
                                         int32_t (*s_bal)[C_LANES], int lane, uint64_t limit) {
         if (!cand) {
-            if (!found || depth == 0)       // no children: leaf => True, root => False
+            // no children: a leaf => True (any' []), the root => False (any []);
+            // a subtree rooted at depth base > 0 is an inner node of the reference tree
+            if (!found || depth == base)
                 return (!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE;
             // ---- backtrack: restore the parent level exactly
             --depth;
@@ -318,7 +324,7 @@ struct LaneDFS {
             const uint32_t gone = ~rem & same_pid(j);
             rem |= (1u << (31 - __builtin_clz(gone & INV))) | (1u << (31 - __builtin_clz(gone & RESP)));
             if constexpr (BANK) {
-                const uint32_t cj = s_ev[j][lane];
+                const uint32_t cj = evc[j * STRIDE];
                 const uint32_t code = c_code(cj), ia = c_a(cj), ib = c_b(cj);
                 const int32_t m = c_val(cj);
                 const uint32_t pa = (st >> 5) & 1u, pb = (st >> 6) & 1u;
@@ -351,7 +357,7 @@ struct LaneDFS {
         const uint32_t rr = rem & pmj & RESP;
         const bool has = rr != 0u;             // findResponse => [] : no child
         const uint32_t r = (uint32_t)__builtin_ctz(rr | 0x80000000u);
-        const uint32_t cj = s_ev[j][lane], cr = s_ev[r][lane];
+        const uint32_t cj = evc[j * STRIDE], cr = evc[r * STRIDE];
         const uint32_t code = c_code(cj), rc = c_code(cr);
         const int32_t m = c_val(cj), rv = c_val(cr);
         bool ok, err;
@@ -536,7 +542,7 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
         } else {
             dfs.init(s, a, s_bal, lane);
             uint32_t iter = 0;
-            while ((status = dfs.step(a, s_ev, s_bal, lane, limit)) < 0) {
+            while ((status = dfs.template step<C_LANES>(a, &s_ev[0][lane], s_bal, lane, limit)) < 0) {
                 if (((iter + 1u) & 1023u) == 0u && beyond_first_fail(a, h)) {
                     status = QSMD_STATUS_SKIPPED;
                     break;
@@ -593,7 +599,7 @@ __global__ __launch_bounds__(C_LANES) void refill_search(SearchArgs a) {
     const uint32_t count = *a.list_count;
     Counters cnt;
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
-    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
+    const uint64_t limit = stage_limit(a);
     bool busy = false, exhausted = false;
     uint32_t h = 0, iter = 0, n_ev = 0, ev_off = 0;
     LaneDFS<MODEL> dfs;
@@ -623,16 +629,19 @@ __global__ __launch_bounds__(C_LANES) void refill_search(SearchArgs a) {
                 }
             }
         }
-        if (__ballot(busy) == 0) break;
+        if (exhausted && __ballot(busy) == 0) break;
         if (busy) {
-            int status = dfs.step(a, s_ev, s_bal, lane, limit);
+            int status = dfs.template step<C_LANES>(a, &s_ev[0][lane], s_bal, lane, limit);
             if (status < 0 && ((iter + 1u) & 1023u) == 0u && beyond_first_fail(a, h))
                 status = QSMD_STATUS_SKIPPED;
             if (status < 0 && time_up(a, t0, iter)) {
                 atomicOr(a.timed_out, 1u);
                 status = QSMD_STATUS_BUDGET;
             }
-            if (status >= 0) {
+            if (status >= 0 && to_split(a, status, dfs.nodes)) {   // -> split stage
+                a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
+                busy = false;
+            } else if (status >= 0) {
                 note_failure(a, h, status);
                 a.status[h] = (uint8_t)status;
                 if (a.nodes) a.nodes[h] = dfs.nodes;

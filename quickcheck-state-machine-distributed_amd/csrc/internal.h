@@ -50,7 +50,108 @@ struct SearchArgs {
     // non-linearisable (or raising); histories above it may stop early and
     // are reported SKIPPED by early_exit_fixup.  Null when the flag is off.
     uint32_t* first_fail;
+    // split stage (csrc/split.hip): a history whose per-lane search reaches
+    // split_budget nodes (< max_nodes) is appended to giant_list and searched
+    // again by many lanes.  Null giant_list = no split.
+    uint32_t* giant_list;
+    uint32_t* giant_count;
+    uint64_t split_budget;
 };
+
+// The per-lane node limit of a stage, and whether reaching it hands the
+// history to the split stage (rather than being the caller's BUDGET).
+__device__ __forceinline__ bool split_enabled(const SearchArgs& a) {
+    return a.giant_list && a.split_budget && (!a.max_nodes || a.split_budget < a.max_nodes);
+}
+__device__ __forceinline__ uint64_t stage_limit(const SearchArgs& a) {
+    return split_enabled(a) ? a.split_budget : (a.max_nodes ? a.max_nodes : ~0ull);
+}
+__device__ __forceinline__ bool to_split(const SearchArgs& a, int status, uint64_t nodes) {
+    return status == QSMD_STATUS_BUDGET && split_enabled(a) && nodes >= a.split_budget;
+}
+
+// ------------------------------------------------------------ split stage
+// One history searched by many lanes.  The frontier kernel
+// runs the reference DFS with a cut at depth D: every node reached at depth D
+// roots a task (its subtree), listed in the reference's DFS order with the
+// number of nodes the reference counts up to and including that node.  The
+// task kernel searches the subtrees in parallel; the combine kernel folds
+// them back in DFS order, so verdict, node count and witness are exactly
+// those of the single DFS.
+enum { SPLIT_VARIANTS = 2 };          // 0: <= 64 events, <= 8 pids; 1: <= 128 events
+constexpr uint32_t kTaskWitness = 64; // bytes per task witness row (<= 64 levels)
+
+struct GiantRec {
+    uint32_t h;             // history index
+    uint32_t variant;       // SPLIT_VARIANTS index, ~0u = not (yet) handled
+    uint32_t first;         // first task, index into the variant's task region
+    uint32_t n_tasks;
+    uint32_t depth;         // cut depth D
+    uint32_t term_status;   // how the search above the cut ended (NONLIN = exhausted)
+    uint64_t term_nodes;    // nodes counted above the cut when it ended
+    uint32_t min_win;       // smallest local task index that decided (LIN / MODEL_ERROR)
+    uint32_t pad;
+};
+
+struct SplitArgs {
+    SearchArgs s;                 // histories, model0, flags, per-history outputs
+    const uint32_t* giant_list;   // giant g = history giant_list[g]
+    const uint32_t* giant_count;
+    GiantRec* giants;
+    qsmd_task* tasks;             // [SPLIT_VARIANTS][task_cap]
+    uint32_t* task_count;         // [SPLIT_VARIANTS]
+    uint32_t* queue_head;         // [SPLIT_VARIANTS]
+    uint32_t task_cap;
+    uint32_t target;              // wanted tasks per giant
+    uint32_t max_tasks;           // tasks per giant at most
+    uint32_t max_depth;           // cut depth at most (<= QSMD_SPLIT_MAX_DEPTH)
+    uint8_t* task_status;         // [SPLIT_VARIANTS][task_cap]
+    uint64_t* task_nodes;
+    uint8_t* task_witness;        // [SPLIT_VARIANTS][task_cap][kTaskWitness] or null
+    unsigned long long* memo;     // QSMD_FLAG_MEMO table (8 x u64 per entry) or null
+    uint64_t memo_mask;           // entries - 1
+    uint32_t external_tasks;      // tasks given by the caller (qsmd_check_tasks)
+};
+
+// Ordered fold of task results (reference DFS order); shared by the combine
+// kernel and qsmd_combine_tasks.  Returns the status, sets nodes and the
+// winning task (-1 if the decision came from above the cut).
+__host__ __device__ inline int combine_tasks(uint32_t term_status, uint64_t term_nodes, const qsmd_task* tasks,
+                                             const uint8_t* st, const uint64_t* nd, uint64_t n,
+                                             uint64_t max_nodes, uint64_t* nodes_out, int64_t* winner) {
+    const uint64_t limit = max_nodes ? max_nodes : ~0ull;
+    uint64_t sum = 0;
+    *winner = -1;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t s = st[i];
+        if (s == QSMD_STATUS_SKIPPED || s == QSMD_STATUS_BUDGET || s > QSMD_STATUS_SKIPPED) {
+            *nodes_out = max_nodes && s == QSMD_STATUS_BUDGET ? max_nodes : tasks[i].top_before + sum;
+            return s == QSMD_STATUS_SKIPPED ? QSMD_STATUS_SKIPPED : QSMD_STATUS_BUDGET;
+        }
+        const uint64_t total = tasks[i].top_before + sum + nd[i];
+        if (total > limit) {
+            *nodes_out = limit;
+            return QSMD_STATUS_BUDGET;
+        }
+        sum += nd[i];
+        if (s == QSMD_STATUS_LINEARISABLE || s == QSMD_STATUS_MODEL_ERROR) {
+            *nodes_out = total;
+            *winner = (int64_t)i;
+            return (int)s;
+        }
+    }
+    if (term_status == QSMD_STATUS_BUDGET) {
+        *nodes_out = max_nodes ? max_nodes : term_nodes + sum;
+        return QSMD_STATUS_BUDGET;
+    }
+    const uint64_t total = term_nodes + sum;
+    if (total > limit) {
+        *nodes_out = limit;
+        return QSMD_STATUS_BUDGET;
+    }
+    *nodes_out = total;
+    return (int)term_status;
+}
 
 // Early exit: relaxed agent-scope read (a stale value only delays skipping).
 __device__ __forceinline__ bool beyond_first_fail(const SearchArgs& a, uint32_t h) {
@@ -75,5 +176,11 @@ uint32_t stage_max_events(int stage);
 
 hipError_t launch_reduce(const unsigned long long* partials, uint64_t n_blocks,
                          qsmd_totals* totals, hipStream_t s);
+
+// Split stage (csrc/split.hip).
+hipError_t launch_frontier(int variant, const SplitArgs& p, uint32_t grid, hipStream_t s);
+hipError_t launch_tasks(int variant, const SplitArgs& p, uint32_t grid, hipStream_t s);
+hipError_t launch_combine(const SplitArgs& p, uint32_t grid, hipStream_t s);
+uint32_t split_lanes(int variant);
 
 }  // namespace qsmd

@@ -65,6 +65,7 @@ __global__ __launch_bounds__(LANES) void lane_search(SearchArgs a) {
     uint32_t c_lin = 0, c_nonlin = 0, c_err = 0, c_enc = 0, c_budget = 0;
     uint64_t c_nodes = 0;
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t limit = stage_limit(a);
 
     for (uint64_t base = (uint64_t)blockIdx.x * LANES; base < total;
          base += (uint64_t)gridDim.x * LANES) {
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(LANES) void lane_search(SearchArgs a) {
                 const MaskT rr = rem & pm & RESP;
                 if (!Ops::any(rr)) continue;            // findResponse => []: no child
                 found = true;
-                if (a.max_nodes && nodes >= a.max_nodes) { status = QSMD_STATUS_BUDGET; break; }
+                if (nodes >= limit) { status = QSMD_STATUS_BUDGET; break; }
                 ++nodes;
                 const int r = Ops::ctz(rr);
                 const uint2 xr = s_ev[r][lane];
@@ -262,7 +263,11 @@ __global__ __launch_bounds__(LANES) void lane_search(SearchArgs a) {
             }
         }
 
-        // ---- outputs
+        // ---- outputs (over the split budget: searched again by the split stage)
+        if (to_split(a, status, nodes)) {
+            a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
+            continue;
+        }
         note_failure(a, h, status);
         a.status[h] = (uint8_t)status;
         if (a.nodes) a.nodes[h] = nodes;

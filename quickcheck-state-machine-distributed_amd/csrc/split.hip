@@ -1,0 +1,696 @@
+// split.hip -- the split stage: one history searched by many lanes
+// (SURVEY.md §8e), and the QSMD_FLAG_MEMO state table.
+//
+// A per-lane search runs as long as its history needs; a wavefront runs as
+// long as its slowest lane.  Heavy-tailed batches (the 10M Bank batch with
+// injected bugs: most histories need tens of nodes, a few need 10^4-10^5)
+// therefore hand every history whose per-lane search reaches the split
+// budget to this stage:
+//
+//   frontier_search  one lane per giant history.  Runs the reference DFS
+//                    (src/Linearisability.hs:52-69, Lemma L1 state) with a
+//                    cut at depth D: a node reached at depth D (a passed
+//                    postcondition, i.e. a `step` that recurses) is not
+//                    expanded but recorded as a task -- its path and the
+//                    number of nodes the reference has counted up to and
+//                    including it.  D is the smallest depth giving `target`
+//                    tasks (count-only passes, then one emitting pass into a
+//                    contiguous reserved range).
+//   task_search      persistent wavefronts; idle lanes pull tasks with one
+//                    atomic per wavefront.  A lane replays the task's path
+//                    (transitions only, nothing counted), then searches the
+//                    subtree below it (`any' (step ...)`: no children = True).
+//                    A task that decides (True, or Map.! raising) lowers the
+//                    giant's min_win; tasks after it are skipped.
+//   combine_giants   one lane per giant folds the task results in DFS order
+//                    (combine_tasks, internal.h): the reference's count is
+//                    nodes above the cut up to the deciding task + all nodes
+//                    of the subtrees before it + that subtree's count.
+//
+// Memo (north star (c)): with QSMD_FLAG_MEMO, a subtree root state (remaining
+// events, model) that was fully searched without success is inserted into an
+// open-addressing table in HBM; a lane that reaches a state in the table
+// skips its subtree.  A state's outcome is a function of the state alone
+// (Lemma L1; post and next read only the model), so pruning never changes a
+// verdict.  Entries are 8 x u64: word 0 = tag (giant id, hash, ready bit),
+// words 1-7 = the exact key; writers store the key with agent-scope (sc1)
+// stores, drain them, then set the ready bit; readers compare every key word,
+// so a stale or torn read can only miss.
+//
+// Generic DFS (GenDFS) over MaskT event bitsets, history in LDS [slot][lane];
+// two variants: <= 64 events / <= 8 pids (u64 masks, 64 lanes) and <= 128
+// events / <= 128 pids (128-bit masks, 16 lanes).
+#include <hip/hip_runtime.h>
+
+#include "internal.h"
+#include "mask.h"
+#include "models.h"
+
+namespace qsmd {
+
+namespace {
+
+constexpr int kDescended = -2;   // step(): descended into a new node
+
+__device__ __forceinline__ uint32_t sp_lane_prefix(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return x;
+}
+
+__device__ __forceinline__ uint64_t ld_sc1(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(unsigned long long* p, uint64_t v) {
+    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// --------------------------------------------------------------- memo table
+constexpr int kMemoKey = 7;       // key words per entry (after the tag)
+constexpr int kMemoProbe = 16;
+
+struct MemoKey {
+    uint64_t w[kMemoKey];
+    uint64_t tag, hash;
+    bool ok;                      // false: state not representable (no memo)
+};
+
+struct Memo {
+    unsigned long long* tab;
+    uint64_t mask;
+
+    __device__ bool lookup(const MemoKey& k) const {
+        for (int i = 0; i < kMemoProbe; ++i) {
+            const unsigned long long* e = tab + ((k.hash + (uint64_t)i) & mask) * 8u;
+            const uint64_t t = ld_sc1(e);
+            if (t == 0) return false;
+            if ((t | 1ull) != (k.tag | 1ull) || !(t & 1ull)) continue;
+            bool eq = true;
+#pragma unroll
+            for (int q = 0; q < kMemoKey; ++q) eq = eq & (ld_sc1(e + 1 + q) == k.w[q]);
+            if (eq) return true;
+        }
+        return false;
+    }
+
+    __device__ void insert(const MemoKey& k) const {
+        for (int i = 0; i < kMemoProbe; ++i) {
+            unsigned long long* e = tab + ((k.hash + (uint64_t)i) & mask) * 8u;
+            uint64_t t = ld_sc1(e);
+            if (t == 0) {
+                t = atomicCAS(e, 0ull, (unsigned long long)k.tag);
+                if (t == 0) {
+#pragma unroll
+                    for (int q = 0; q < kMemoKey; ++q) st_sc1(e + 1 + q, k.w[q]);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_fetch_or(e, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    return;
+                }
+            }
+            if ((t | 1ull) == (k.tag | 1ull)) {
+                if (!(t & 1ull)) return;          // being written (likely this very key)
+                bool eq = true;
+#pragma unroll
+                for (int q = 0; q < kMemoKey; ++q) eq = eq & (ld_sc1(e + 1 + q) == k.w[q]);
+                if (eq) return;
+            }
+        }
+    }
+};
+
+// ----------------------------------------------------------- generic DFS
+
+template <uint32_t MODEL, typename MaskT, int MAXEV, int MAXPID, int LANES>
+struct GLds {
+    static constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
+    static constexpr int MAXD = MAXEV / 2;
+    uint2 ev[MAXEV][LANES];
+    MaskT pm[MAXPID][LANES];
+    uint32_t meta[MAXD][LANES];                         // j | pre-op model bits
+    int64_t undo[BANK ? 1 : MAXD][LANES];               // Ticket: pre-op n
+    int64_t bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][LANES];
+};
+
+template <typename MaskT> __device__ __forceinline__ uint64_t mask_lo(const MaskT& m) { return (uint64_t)m; }
+template <typename MaskT> __device__ __forceinline__ uint64_t mask_hi(const MaskT&) { return 0ull; }
+template <> __device__ __forceinline__ uint64_t mask_lo<M128>(const M128& m) { return m.lo; }
+template <> __device__ __forceinline__ uint64_t mask_hi<M128>(const M128& m) { return m.hi; }
+
+template <uint32_t MODEL, typename MaskT, int MAXEV, int MAXPID, int LANES>
+struct GenDFS {
+    using Ops = MaskOps<MaskT>;
+    using Lds = GLds<MODEL, MaskT, MAXEV, MAXPID, LANES>;
+    static constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
+
+    MaskT INV, RESP, rem, cand;
+    uint32_t depth, base, found, skip_ins, n_ev;
+    uint64_t nodes;
+    BankState bank;
+    TicketState tick;
+
+    // Stage history H into the lane's LDS column and validate it.
+    __device__ bool load(const SearchArgs& a, const qsmd_hdr& H, Lds& s, int lane) {
+        n_ev = H.n_ev;
+        const uint32_t n_pid = H.n_pid;
+        INV = MaskT{};
+        RESP = MaskT{};
+        bool ok = H.model_id == MODEL && n_ev <= (uint32_t)MAXEV && n_pid <= (uint32_t)MAXPID &&
+                  (uint64_t)H.ev_off + n_ev <= a.n_events;
+        if (!ok) return false;
+        for (uint32_t p = 0; p < n_pid; ++p) s.pm[p][lane] = MaskT{};
+        const uint2* evp = a.events + H.ev_off;
+        for (uint32_t e0 = 0; e0 < n_ev; e0 += 8) {
+            uint2 xs[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) xs[k] = e0 + k < n_ev ? evp[e0 + k] : make_uint2(0u, 0u);
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t e = e0 + k;
+                if (e >= n_ev) break;
+                const Ev ev{xs[k].x, (int32_t)xs[k].y};
+                const uint32_t p = ev.pid();
+                ok = ok && p < n_pid && valid_event<MODEL>(ev);
+                s.ev[e][lane] = xs[k];
+                const MaskT bit = Ops::bit((int)e);
+                if (ev.is_resp()) RESP |= bit; else INV |= bit;
+                if (p < n_pid) s.pm[p][lane] = s.pm[p][lane] | bit;
+            }
+        }
+        return ok;
+    }
+
+    __device__ __forceinline__ MaskT candidates(const MaskT& r) const {
+        const MaskT rr = r & RESP;
+        const int R = Ops::any(rr) ? Ops::ctz(rr) : Ops::BITS;
+        return r & INV & Ops::below(R);
+    }
+
+    // model0 and the root of the search
+    __device__ void init(const SearchArgs& a, Lds& s, int lane) {
+        bank = BankState{a.m0_exists, 0u};
+        tick = TicketState{a.m0_just, a.m0_val[0]};
+        if constexpr (BANK) {
+#pragma unroll
+            for (int c = 0; c < QSMD_BANK_MAX_ACCOUNTS; ++c) {
+                const bool ex = (a.m0_exists >> c) & 1u;
+                const int64_t v = ex ? a.m0_val[c] : 0;
+                s.bal[c][lane] = v;
+                bank.neg |= (ex && v < 0) ? (1u << c) : 0u;
+            }
+        }
+        rem = INV | RESP;
+        cand = candidates(rem);
+        depth = 0;
+        base = 0;
+        found = 0;
+        skip_ins = 0;
+        nodes = 0;
+    }
+
+    // Push level `depth` for child j (its response r) and apply the
+    // transition (Left inv; Right is the identity for both models).
+    __device__ __forceinline__ void descend(uint32_t j, const Ev& ej, const MaskT& pm, int r, Lds& s, int lane) {
+        if constexpr (BANK) {
+            s.meta[depth][lane] = j | (bank.exists << 8) | (bank.neg << 16);
+            const uint32_t code = ej.code();
+            if (code != QSMD_BANK_CHECK_BALANCE) {
+                const int ia = (int)ej.a();
+                const int64_t m = ej.val;
+                const bool ex_a = (bank.exists >> ia) & 1u;
+                const int64_t bal_a = s.bal[ia][lane];
+                int64_t na;
+                if (code == QSMD_BANK_OPEN_ACCOUNT) na = ex_a ? bal_a : 0;
+                else if (code == QSMD_BANK_DEPOSIT) na = ex_a ? bal_a + m : m;
+                else na = ex_a ? bal_a - m : m;          // Withdraw / Transfer's withdraw
+                s.bal[ia][lane] = na;
+                bank.exists |= 1u << ia;
+                bank.neg = (bank.neg & ~(1u << ia)) | (na < 0 ? (1u << ia) : 0u);
+                if (code == QSMD_BANK_TRANSFER) {
+                    const int ib = (int)ej.b();
+                    const bool ex_b = (bank.exists >> ib) & 1u;
+                    const int64_t nb = ex_b ? s.bal[ib][lane] + m : m;
+                    s.bal[ib][lane] = nb;
+                    bank.exists |= 1u << ib;
+                    bank.neg = (bank.neg & ~(1u << ib)) | (nb < 0 ? (1u << ib) : 0u);
+                }
+            }
+        } else {
+            s.meta[depth][lane] = j | (tick.just << 8);
+            s.undo[depth][lane] = tick.n;
+            ticket_apply(tick, ej);
+        }
+        ++depth;
+        rem &= ~(Ops::lowest(rem & pm & INV) | Ops::bit(r));
+        cand = candidates(rem);
+        found = 0;
+    }
+
+    // Pop level depth-1 and restore its state exactly; the remaining
+    // candidates of that level are the ones after j.
+    __device__ __forceinline__ void backtrack(Lds& s, int lane) {
+        --depth;
+        const uint32_t meta = s.meta[depth][lane];
+        const uint32_t j = meta & 0xFFu;
+        const uint2 xj = s.ev[j][lane];
+        const Ev ej{xj.x, (int32_t)xj.y};
+        const MaskT gone = ~rem & s.pm[ej.pid()][lane];
+        rem |= Ops::bit(Ops::msb(gone & INV)) | Ops::bit(Ops::msb(gone & RESP));
+        if constexpr (BANK) {
+            const uint32_t code = ej.code();
+            if (code != QSMD_BANK_CHECK_BALANCE) {
+                const uint32_t pre_ex = (meta >> 8) & 0xFFu;
+                const int ia = (int)ej.a();
+                const int64_t m = ej.val;
+                if (code == QSMD_BANK_TRANSFER) {
+                    const int ib = (int)ej.b();
+                    const bool exb_mid = ((pre_ex | (1u << ia)) >> ib) & 1u;
+                    s.bal[ib][lane] = exb_mid ? s.bal[ib][lane] - m : 0;
+                }
+                const int64_t delta = code == QSMD_BANK_DEPOSIT ? m : code == QSMD_BANK_OPEN_ACCOUNT ? 0 : -m;
+                s.bal[ia][lane] = ((pre_ex >> ia) & 1u) ? s.bal[ia][lane] - delta : 0;
+                bank.exists = pre_ex;
+                bank.neg = (meta >> 16) & 0xFFu;
+            }
+        } else {
+            tick.just = (meta >> 8) & 1u;
+            tick.n = s.undo[depth][lane];
+        }
+        cand = candidates(rem) & ~Ops::below((int)j + 1);
+        found = 1;
+    }
+
+    // Follow a recorded choice without evaluating or counting it.
+    __device__ __forceinline__ void replay(uint32_t j, Lds& s, int lane) {
+        const uint2 xj = s.ev[j][lane];
+        const Ev ej{xj.x, (int32_t)xj.y};
+        const MaskT pm = s.pm[ej.pid()][lane];
+        const MaskT rr = rem & pm & RESP;
+        descend(j, ej, pm, Ops::ctz(rr), s, lane);
+    }
+
+    // The state key (remaining events, model) for the memo table.
+    __device__ MemoKey key(uint32_t id, Lds& s, int lane) const {
+        MemoKey k;
+        k.ok = true;
+        k.w[0] = mask_lo(rem);
+        k.w[1] = mask_hi(rem);
+        if constexpr (BANK) {
+            k.w[2] = bank.exists;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t b0 = ((bank.exists >> (2 * q)) & 1u) ? s.bal[2 * q][lane] : 0;
+                const int64_t b1 = ((bank.exists >> (2 * q + 1)) & 1u) ? s.bal[2 * q + 1][lane] : 0;
+                k.ok = k.ok && b0 == (int64_t)(int32_t)b0 && b1 == (int64_t)(int32_t)b1;
+                k.w[3 + q] = (uint64_t)(uint32_t)(int32_t)b0 | ((uint64_t)(uint32_t)(int32_t)b1 << 32);
+            }
+        } else {
+            k.w[2] = tick.just;
+            k.w[3] = tick.just ? (uint64_t)tick.n : 0ull;
+            k.w[4] = k.w[5] = k.w[6] = 0;
+        }
+        uint64_t h = mix64(0x51ED5EEDull + id);
+#pragma unroll
+        for (int q = 0; q < kMemoKey; ++q) h = mix64(h ^ k.w[q]);
+        k.hash = h;
+        k.tag = ((uint64_t)(id + 1u) << 32) | ((h >> 32) & 0xFFFFFFFEull);
+        return k;
+    }
+
+    // One DFS iteration.  Returns -1 (continue), kDescended (a node passed
+    // its postcondition and was entered), or the final QSMD_STATUS_*.
+    template <bool MEMO>
+    __device__ int step(Lds& s, int lane, uint64_t limit, const Memo& memo, uint32_t id) {
+        if (!Ops::any(cand)) {
+            // no children: a leaf => True (any' []), the root => False (any []);
+            // a subtree rooted at depth base > 0 is an inner node of the tree
+            if (!found || depth == base) {
+                if constexpr (MEMO) {
+                    if (found && depth > 0 && !skip_ins) {   // a task root that failed
+                        const MemoKey k = key(id, s, lane);
+                        if (k.ok) memo.insert(k);
+                    }
+                }
+                return (!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE;
+            }
+            if constexpr (MEMO) {
+                if (!skip_ins) {
+                    const MemoKey k = key(id, s, lane);      // this state failed
+                    if (k.ok) memo.insert(k);
+                }
+                skip_ins = 0;
+            }
+            backtrack(s, lane);
+            return -1;
+        }
+        const uint32_t j = (uint32_t)Ops::ctz(cand);
+        cand = Ops::clear_lowest(cand);
+        const uint2 xj = s.ev[j][lane];
+        const Ev ej{xj.x, (int32_t)xj.y};
+        const MaskT pm = s.pm[ej.pid()][lane];
+        const MaskT rr = rem & pm & RESP;
+        if (!Ops::any(rr)) return -1;                  // findResponse => []: no child
+        found = 1;
+        if (nodes >= limit) return QSMD_STATUS_BUDGET;
+        ++nodes;
+        const int r = Ops::ctz(rr);
+        const uint2 xr = s.ev[r][lane];
+        const Ev er{xr.x, (int32_t)xr.y};
+        int post;
+        if constexpr (BANK) post = bank_post(bank, ej, er, s.bal[ej.a()][lane]);
+        else post = ticket_post(tick, ej, er);
+        if (post == POST_ERROR) return QSMD_STATUS_MODEL_ERROR;
+        if (post == POST_FALSE) return -1;
+        descend(j, ej, pm, r, s, lane);
+        if constexpr (MEMO) {
+            const MemoKey k = key(id, s, lane);
+            if (k.ok && memo.lookup(k)) {              // known to fail: skip the subtree
+                cand = MaskT{};
+                found = 1;
+                skip_ins = 1;
+            }
+        }
+        return kDescended;
+    }
+
+    // Abandon the node just entered as if its subtree had failed (the cut).
+    __device__ __forceinline__ void prune() {
+        cand = MaskT{};
+        found = 1;
+        skip_ins = 1;
+    }
+
+    __device__ void path_to(uint8_t* w, uint32_t len, Lds& s, int lane) const {
+        for (uint32_t d = 0; d < depth && d < len; ++d) w[d] = (uint8_t)(s.meta[d][lane] & 0xFFu);
+        if (depth < len) w[depth] = QSMD_WITNESS_END;
+    }
+};
+
+__device__ __forceinline__ bool sp_time_up(const SearchArgs& a, uint64_t t0, uint32_t iter) {
+    return a.time_limit && ((iter & 1023u) == 0u) && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit;
+}
+
+template <int MAXEV, int MAXPID>
+__device__ __forceinline__ bool fits_variant(const qsmd_hdr& H) {
+    return H.n_ev <= (uint32_t)MAXEV && H.n_pid <= (uint32_t)MAXPID;
+}
+// variant of a history: the first that holds it (0: <= 64 events, <= 8 pids)
+__device__ __forceinline__ uint32_t variant_of(const qsmd_hdr& H) {
+    return fits_variant<64, 8>(H) ? 0u : 1u;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- frontier
+
+// Search above the cut.  Returns the terminal status; count = tasks reached
+// (written to out[0..) when out != null); top = nodes counted.
+template <uint32_t MODEL, typename MaskT, int MAXEV, int MAXPID, int LANES>
+__device__ int top_search(GenDFS<MODEL, MaskT, MAXEV, MAXPID, LANES>& d,
+                          GLds<MODEL, MaskT, MAXEV, MAXPID, LANES>& s, const SearchArgs& a, int lane,
+                          uint32_t cut, uint64_t limit, uint32_t g, uint32_t max_count, qsmd_task* out,
+                          uint32_t& count, uint64_t t0) {
+    const Memo none{nullptr, 0};
+    d.init(a, s, lane);
+    count = 0;
+    uint32_t iter = 0;
+    for (;;) {
+        const int st = d.template step<false>(s, lane, limit, none, 0);
+        if (st == kDescended) {
+            if (d.depth == cut) {
+                if (out && count < max_count) {
+                    qsmd_task t;
+                    t.hist = g;
+                    t.depth = (uint16_t)cut;
+                    t.reserved = 0;
+                    t.top_before = d.nodes;
+#pragma unroll
+                    for (int q = 0; q < QSMD_SPLIT_MAX_DEPTH; ++q)
+                        t.path[q] = (uint32_t)q < cut ? (uint8_t)(s.meta[q][lane] & 0xFFu) : (uint8_t)0;
+                    out[count] = t;
+                }
+                ++count;
+                d.prune();
+            }
+            continue;
+        }
+        if (st >= 0) return st;
+        if (sp_time_up(a, t0, ++iter)) {
+            atomicOr(a.timed_out, 1u);
+            return QSMD_STATUS_BUDGET;
+        }
+    }
+}
+
+template <uint32_t MODEL, typename MaskT, int MAXEV, int MAXPID, int LANES>
+__global__ __launch_bounds__(LANES) void frontier_search(SplitArgs p, uint32_t variant) {
+    using DFS = GenDFS<MODEL, MaskT, MAXEV, MAXPID, LANES>;
+    __shared__ GLds<MODEL, MaskT, MAXEV, MAXPID, LANES> s;
+    const SearchArgs& a = p.s;
+    const int lane = threadIdx.x;
+    const uint32_t n_g = *p.giant_count;
+    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
+    const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
+    for (uint32_t g = blockIdx.x * LANES + lane; g < n_g; g += gridDim.x * LANES) {
+        const uint32_t h = p.giant_list[g];
+        const qsmd_hdr H = a.hdr[h];
+        if (variant_of(H) != variant) continue;
+        GiantRec G;
+        G.h = h;
+        G.variant = variant;
+        G.first = 0;
+        G.n_tasks = 0;
+        G.depth = 0;
+        G.term_status = QSMD_STATUS_ENCODE_ERROR;
+        G.term_nodes = 0;
+        G.min_win = ~0u;
+        G.pad = 0;
+        DFS d;
+        if (!d.load(a, H, s, lane)) {
+            p.giants[g] = G;
+            continue;
+        }
+        if (d.n_ev == 0) {
+            G.term_status = QSMD_STATUS_LINEARISABLE;             // :59
+            p.giants[g] = G;
+            continue;
+        }
+        const uint32_t dmax = min(min(p.max_depth, (uint32_t)QSMD_SPLIT_MAX_DEPTH), d.n_ev / 2u);
+        uint32_t cut = 1, count = 0;
+        for (;; ++cut) {
+            top_search(d, s, a, lane, cut, limit, g, 0, nullptr, count, t0);
+            if (count > p.max_tasks && cut > 1) { --cut; break; }
+            if (count >= p.target || cut >= dmax) break;
+        }
+        // reserve a contiguous range; on overflow search the whole history here
+        qsmd_task* region = p.tasks + (uint64_t)variant * p.task_cap;
+        uint32_t first = ~0u;
+        top_search(d, s, a, lane, cut, limit, g, 0, nullptr, count, t0);
+        if (count <= p.max_tasks) {
+            first = atomicAdd(&p.task_count[variant], count);
+            if ((uint64_t)first + count > p.task_cap) first = ~0u;
+        }
+        int st;
+        if (first != ~0u) {
+            uint32_t emitted = 0;
+            st = top_search(d, s, a, lane, cut, limit, g, count, region + first, emitted, t0);
+            G.first = first;
+            G.n_tasks = count;
+            G.depth = cut;
+        } else {
+            const Memo none{nullptr, 0};
+            d.init(a, s, lane);
+            uint32_t iter = 0;
+            while ((st = d.template step<false>(s, lane, limit, none, 0)) < 0) {
+                if (sp_time_up(a, t0, ++iter)) {
+                    atomicOr(a.timed_out, 1u);
+                    st = QSMD_STATUS_BUDGET;
+                    break;
+                }
+            }
+        }
+        G.term_status = (uint32_t)st;
+        G.term_nodes = d.nodes;
+        if (a.witness && st == QSMD_STATUS_LINEARISABLE) d.path_to(a.witness + H.ev_off, d.n_ev, s, lane);
+        p.giants[g] = G;
+    }
+}
+
+// ------------------------------------------------------------------- tasks
+
+template <uint32_t MODEL, typename MaskT, int MAXEV, int MAXPID, int LANES>
+__global__ __launch_bounds__(LANES) void task_search(SplitArgs p, uint32_t variant) {
+    using DFS = GenDFS<MODEL, MaskT, MAXEV, MAXPID, LANES>;
+    constexpr uint32_t kRefillMin = LANES >= 64 ? 8u : 2u;
+    __shared__ GLds<MODEL, MaskT, MAXEV, MAXPID, LANES> s;
+    const SearchArgs& a = p.s;
+    const int lane = threadIdx.x;
+    const uint32_t count = min(*(volatile uint32_t*)&p.task_count[variant], p.task_cap);
+    const qsmd_task* tasks = p.tasks + (uint64_t)variant * p.task_cap;
+    uint8_t* t_status = p.task_status + (uint64_t)variant * p.task_cap;
+    uint64_t* t_nodes = p.task_nodes + (uint64_t)variant * p.task_cap;
+    uint8_t* t_wit = p.task_witness ? p.task_witness + (uint64_t)variant * p.task_cap * kTaskWitness : nullptr;
+    const Memo memo{p.memo, p.memo_mask};
+    const bool use_memo = p.memo != nullptr;
+    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
+    const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
+
+    bool busy = false, exhausted = count == 0;
+    uint32_t idx = 0, g = 0, local = 0, h = 0, iter = 0;
+    DFS d;
+    d.depth = 0;
+    d.nodes = 0;
+    for (;;) {
+        const uint64_t idle = __ballot(!busy);
+        const uint64_t busy_m = __ballot(busy);
+        if (exhausted && busy_m == 0) break;
+        if (!exhausted && idle && (__builtin_popcountll(idle) >= kRefillMin || busy_m == 0)) {
+            const int leader = __builtin_ctzll(idle);
+            const uint32_t want = (uint32_t)__builtin_popcountll(idle);
+            uint32_t first = 0;
+            if (lane == leader) first = atomicAdd(&p.queue_head[variant], want);
+            first = __shfl(first, leader, LANES);
+            if (first + want >= count) exhausted = true;
+            if (!busy) {
+                idx = first + sp_lane_prefix(idle);
+                if (idx < count) {
+                    const qsmd_task T = tasks[idx];   // path bytes re-read below (no scratch)
+                    g = T.hist;
+                    const GiantRec* G = p.giants + g;
+                    h = p.external_tasks ? 0u : G->h;
+                    local = idx - G->first;
+                    const uint32_t mw = __hip_atomic_load(&G->min_win, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (local > mw || beyond_first_fail(a, h)) {
+                        t_status[idx] = QSMD_STATUS_SKIPPED;
+                        t_nodes[idx] = 0;
+                    } else {
+                        d.load(a, a.hdr[h], s, lane);         // validated by the frontier
+                        d.init(a, s, lane);
+                        for (uint32_t q = 0; q < T.depth; ++q) d.replay(tasks[idx].path[q], s, lane);
+                        d.base = T.depth;
+                        busy = true;
+                        iter = 0;
+                        if (use_memo && T.depth > 0) {           // root state known to fail
+                            const MemoKey k = d.key(g, s, lane);
+                            if (k.ok && memo.lookup(k)) {
+                                t_status[idx] = QSMD_STATUS_NONLINEARISABLE;
+                                t_nodes[idx] = 0;
+                                busy = false;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        if (busy) {
+            int st = use_memo ? d.template step<true>(s, lane, limit, memo, g)
+                              : d.template step<false>(s, lane, limit, memo, g);
+            if (st < 0 && ((++iter & 1023u) == 0u)) {
+                const uint32_t mw = __hip_atomic_load(&p.giants[g].min_win, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+                if (local > mw || beyond_first_fail(a, h)) st = QSMD_STATUS_SKIPPED;
+                else if (sp_time_up(a, t0, iter)) {
+                    atomicOr(a.timed_out, 1u);
+                    st = QSMD_STATUS_BUDGET;
+                }
+            }
+            if (st >= 0) {
+                t_status[idx] = (uint8_t)st;
+                t_nodes[idx] = st == QSMD_STATUS_SKIPPED ? 0ull : d.nodes;
+                if (st == QSMD_STATUS_LINEARISABLE || st == QSMD_STATUS_MODEL_ERROR)
+                    atomicMin(&p.giants[g].min_win, local);
+                if (t_wit && st == QSMD_STATUS_LINEARISABLE)
+                    d.path_to(t_wit + (uint64_t)idx * kTaskWitness, kTaskWitness, s, lane);
+                busy = false;
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------- combine
+
+__global__ __launch_bounds__(64) void combine_giants(SplitArgs p) {
+    const SearchArgs& a = p.s;
+    const uint32_t n_g = *p.giant_count;
+    uint64_t c[T_N] = {};
+    for (uint32_t g = blockIdx.x * 64 + threadIdx.x; g < n_g; g += gridDim.x * 64) {
+        const GiantRec G = p.giants[g];
+        const uint32_t h = G.h;
+        const uint64_t base = (uint64_t)G.variant * p.task_cap + G.first;
+        uint64_t nodes = 0;
+        int64_t win = -1;
+        const int st = combine_tasks(G.term_status, G.term_nodes, p.tasks + base, p.task_status + base,
+                                     p.task_nodes + base, G.n_tasks, a.max_nodes, &nodes, &win);
+        note_failure(a, h, st);
+        a.status[h] = (uint8_t)st;
+        if (a.nodes) a.nodes[h] = nodes;
+        if (a.witness && win >= 0 && st == QSMD_STATUS_LINEARISABLE) {
+            const uint8_t* row = p.task_witness + (base + (uint64_t)win) * kTaskWitness;
+            const qsmd_hdr H = a.hdr[h];
+            for (uint32_t q = 0; q < H.n_ev && q < kTaskWitness; ++q) {
+                a.witness[H.ev_off + q] = row[q];
+                if (row[q] == QSMD_WITNESS_END) break;
+            }
+        }
+        if (st == QSMD_STATUS_SKIPPED) continue;
+        c[T_LIN] += st == QSMD_STATUS_LINEARISABLE;
+        c[T_NONLIN] += st == QSMD_STATUS_NONLINEARISABLE;
+        c[T_ERR] += st == QSMD_STATUS_MODEL_ERROR;
+        c[T_ENC] += st == QSMD_STATUS_ENCODE_ERROR;
+        c[T_BUDGET] += st == QSMD_STATUS_BUDGET;
+        c[T_NODES] += nodes;
+    }
+    c[T_CHECKED] = c[T_LIN] + c[T_NONLIN] + c[T_ERR];
+#pragma unroll
+    for (int k = 0; k < T_N; ++k) {
+        uint64_t v = c[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (threadIdx.x == 0) a.partials[(uint64_t)blockIdx.x * T_N + k] = v;
+    }
+}
+
+// ------------------------------------------------------------------ launch
+
+namespace {
+template <uint32_t MODEL>
+hipError_t launch_split_model(bool frontier, int variant, const SplitArgs& p, uint32_t grid, hipStream_t s) {
+    if (variant == 0) {
+        if (frontier)
+            hipLaunchKernelGGL((frontier_search<MODEL, uint64_t, 64, 8, 64>), dim3(grid), dim3(64), 0, s, p, 0u);
+        else
+            hipLaunchKernelGGL((task_search<MODEL, uint64_t, 64, 8, 64>), dim3(grid), dim3(64), 0, s, p, 0u);
+    } else {
+        if (frontier)
+            hipLaunchKernelGGL((frontier_search<MODEL, M128, 128, 128, 16>), dim3(grid), dim3(16), 0, s, p, 1u);
+        else
+            hipLaunchKernelGGL((task_search<MODEL, M128, 128, 128, 16>), dim3(grid), dim3(16), 0, s, p, 1u);
+    }
+    return hipGetLastError();
+}
+}  // namespace
+
+uint32_t split_lanes(int variant) { return variant == 0 ? 64u : 16u; }
+
+hipError_t launch_frontier(int variant, const SplitArgs& p, uint32_t grid, hipStream_t s) {
+    if (p.s.model_id == QSMD_MODEL_BANK) return launch_split_model<QSMD_MODEL_BANK>(true, variant, p, grid, s);
+    return launch_split_model<QSMD_MODEL_TICKET>(true, variant, p, grid, s);
+}
+
+hipError_t launch_tasks(int variant, const SplitArgs& p, uint32_t grid, hipStream_t s) {
+    if (p.s.model_id == QSMD_MODEL_BANK) return launch_split_model<QSMD_MODEL_BANK>(false, variant, p, grid, s);
+    return launch_split_model<QSMD_MODEL_TICKET>(false, variant, p, grid, s);
+}
+
+hipError_t launch_combine(const SplitArgs& p, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(combine_giants, dim3(grid), dim3(64), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace qsmd

@@ -26,6 +26,20 @@ class DeviceError(RuntimeError):
     pass
 
 
+QSMD_SPLIT_MAX_DEPTH = 16
+TASK_WITNESS_BYTES = 64
+
+# qsmd_task / qsmd_frontier (include/qsmd.h, split search)
+TASK_DTYPE = np.dtype([("hist", "<u4"), ("depth", "<u2"), ("reserved", "<u2"),
+                       ("top_before", "<u8"), ("path", "u1", (QSMD_SPLIT_MAX_DEPTH,))])
+assert TASK_DTYPE.itemsize == 32
+
+
+class Frontier(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_uint32), ("depth", ctypes.c_uint32),
+                ("top_nodes", ctypes.c_uint64), ("n_tasks", ctypes.c_uint64)]
+
+
 class Totals(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "checked", "linearisable", "nonlinearisable", "model_errors", "encode_errors",
@@ -54,7 +68,29 @@ EXPORTS = {
     "qsmd_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
     "qsmd_timing_reset": (_I, [_P]),
     "qsmd_timing_read": (_I, [_P, _P, _P, _U64, ctypes.POINTER(_U64)]),
+    "qsmd_set_split_budget": (_I, [_P, _U64]),
+    "qsmd_set_memo_capacity": (_I, [_P, _U64]),
+    "qsmd_split_frontier": (_I, [_P, _U32, _P, _P, _U64, _P, _U32, _U64, _U32, _P, _U64, _P, _P]),
+    "qsmd_check_tasks": (_I, [_P, _U32, _P, _P, _U64, _P, _U32, _U64, _P, _U64, _P, _P, _P]),
+    "qsmd_combine_tasks": (_I, [_P, _P, _P, _P, _U64, _U64, _P, _P, _P]),
 }
+
+
+def combine_tasks(frontier, tasks, status, nodes, max_nodes=0):
+    """Fold task results in DFS order (qsmd_combine_tasks: host code of the
+    library, no device).  Returns (status, nodes, winner index or -1)."""
+    lib = load_library()
+    tasks = np.ascontiguousarray(tasks, dtype=TASK_DTYPE)
+    status = np.ascontiguousarray(status, dtype=np.uint8)
+    nodes = np.ascontiguousarray(nodes, dtype=np.uint64)
+    st, nd, win = ctypes.c_uint8(), ctypes.c_uint64(), ctypes.c_int64()
+    n = len(tasks)
+    rc = lib.qsmd_combine_tasks(ctypes.byref(frontier), _ptr(tasks) if n else None,
+                                _ptr(status) if n else None, _ptr(nodes) if n else None, n,
+                                int(max_nodes), ctypes.byref(st), ctypes.byref(nd), ctypes.byref(win))
+    if rc != 0:
+        raise DeviceError(f"qsmd_combine_tasks failed ({rc})")
+    return int(st.value), int(nd.value), int(win.value)
 
 
 def load_library(path=LIB_PATH):
@@ -161,6 +197,55 @@ class Context:
 
     def set_stage0_grid(self, max_blocks):
         self._check(self._lib.qsmd_set_stage0_grid(self._h, int(max_blocks)), "qsmd_set_stage0_grid")
+
+    def set_split_budget(self, nodes):
+        self._check(self._lib.qsmd_set_split_budget(self._h, int(nodes)), "qsmd_set_split_budget")
+
+    def set_memo_capacity(self, entries):
+        self._check(self._lib.qsmd_set_memo_capacity(self._h, int(entries)), "qsmd_set_memo_capacity")
+
+    @staticmethod
+    def _one(hdr, events):
+        hdr = np.ascontiguousarray(hdr, dtype=codec.HDR_DTYPE)
+        events = np.ascontiguousarray(events, dtype=codec.EV_DTYPE)
+        if len(hdr) != 1:
+            raise ValueError("the split search takes exactly one history")
+        return hdr, events
+
+    def split_frontier(self, model_id, hdr, events, model0=None, flags=QSMD_FLAG_EXHAUSTIVE,
+                       max_nodes=0, min_tasks=64, max_tasks=4096, witness=False):
+        """Cut the search of one history (qsmd_split_frontier).
+        Returns (Frontier, tasks TASK_DTYPE[n], witness u8[n_ev] or None)."""
+        hdr, events = self._one(hdr, events)
+        tasks = np.zeros(max(int(max_tasks), 1), dtype=TASK_DTYPE)
+        fr = Frontier()
+        n_ev = int(hdr[0]["n_ev"])
+        wit = np.full(max(n_ev, 1), 0xFF, dtype=np.uint8) if witness else None
+        m0 = ctypes.cast(ctypes.pointer(model0), ctypes.c_void_p) if model0 is not None else None
+        rc = self._lib.qsmd_split_frontier(
+            self._h, model_id, _ptr(hdr), _ptr(events) if len(events) else None, len(events), m0, flags,
+            int(max_nodes), int(min_tasks), _ptr(tasks), int(max_tasks), ctypes.byref(fr),
+            _ptr(wit) if wit is not None else None)
+        self._check(rc, "qsmd_split_frontier")
+        return fr, tasks[: fr.n_tasks].copy(), (wit[:n_ev] if wit is not None else None)
+
+    def check_tasks(self, model_id, hdr, events, tasks, model0=None, flags=QSMD_FLAG_EXHAUSTIVE,
+                    max_nodes=0, witness=False):
+        """Search task subtrees of one history (qsmd_check_tasks).
+        Returns (status u8[n], nodes u64[n], witness u8[n, 64] or None)."""
+        hdr, events = self._one(hdr, events)
+        tasks = np.ascontiguousarray(tasks, dtype=TASK_DTYPE)
+        n = len(tasks)
+        status = np.empty(n, dtype=np.uint8)
+        nodes = np.empty(n, dtype=np.uint64)
+        wit = np.full((n, TASK_WITNESS_BYTES), 0xFF, dtype=np.uint8) if witness else None
+        m0 = ctypes.cast(ctypes.pointer(model0), ctypes.c_void_p) if model0 is not None else None
+        rc = self._lib.qsmd_check_tasks(
+            self._h, model_id, _ptr(hdr), _ptr(events) if len(events) else None, len(events), m0, flags,
+            int(max_nodes), _ptr(tasks) if n else None, n, _ptr(status) if n else None,
+            _ptr(nodes) if n else None, _ptr(wit) if (wit is not None and n) else None)
+        self._check(rc, "qsmd_check_tasks")
+        return status, nodes, wit
 
     def set_stage0_budget(self, nodes):
         self._check(self._lib.qsmd_set_stage0_budget(self._h, int(nodes)), "qsmd_set_stage0_budget")

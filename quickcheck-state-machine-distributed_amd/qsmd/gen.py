@@ -92,6 +92,33 @@ def generate(p, first, n_hist, threads=8, ev_base=0):
     return hdr, events, bug
 
 
+def adversarial_ticket(n_clients=8, n_ops=64, bug=True):
+    """BASELINE config 4: one TicketDispenser history, n_clients x n_ops with
+    the heaviest overlap, every event on the test process's pid (Q1,
+    test/TicketDispenser.hs:302-309).  After a sequential Reset, TakeTickets
+    are invoked n_clients at a time and answered in order.  Every pending
+    TakeTicket is a candidate child with the same successor state, so the
+    reference search tree has (n_clients!)^(n_ops / n_clients) paths; with
+    `bug` the last Number is off by one, the history is non-linearisable and
+    the exhaustive search must visit all of them -- only state memoisation
+    (QSMD_FLAG_MEMO) makes it tractable.  Returns (hdr[1], events, bug[1])."""
+    ev = [(0x00, 1, 0, 0, 0), (0x80, 1, 0, 0, 0)]          # L Reset, R Ok
+    n, left = 0, n_ops - 1
+    while left > 0:
+        w = min(n_clients, left)
+        ev += [(0x00, 0, 0, 0, 0)] * w                     # L TakeTicket
+        ev += [(0x80, 0, 0, 0, n + 1 + i) for i in range(w)]   # R Number
+        n += w
+        left -= w
+    if bug:
+        k, c, a, b, v = ev[-1]
+        ev[-1] = (k, c, a, b, v + 1)
+    events = np.array(ev, dtype=codec.EV_DTYPE)
+    hdr = np.zeros(1, dtype=codec.HDR_DTYPE)
+    hdr[0] = (0, len(ev), 1, MODEL_TICKET, 0, 0)
+    return hdr, events, np.array([1 if bug else 0], dtype=np.uint8)
+
+
 def generate_config(name, first, n_hist, threads=8, **override):
     kw = dict(CONFIGS[name])
     kw.update(override)

@@ -1,0 +1,197 @@
+"""GPU parity of the split stage (csrc/split.hip) and of QSMD_FLAG_MEMO.
+
+The split stage must be invisible in exhaustive mode: a history searched by
+many lanes (frontier -> tasks -> ordered combine) has exactly the verdict,
+node count and witness of the single reference DFS (oracle/ref_cpu.c).  The
+split budget is lowered so that most histories take that path.  With MEMO,
+verdicts and witnesses are exact and node counts never exceed the
+exhaustive ones.
+"""
+
+import contextlib
+import random
+
+import numpy as np
+import pytest
+
+import histgen
+import oracle_c
+from qsmd import codec, device, gen, models
+from test_gpu_parity import _compare
+
+pytestmark = pytest.mark.gpu
+
+DEFAULT_SPLIT = 4096
+EXH = device.QSMD_FLAG_EXHAUSTIVE
+MEMO = device.QSMD_FLAG_MEMO
+
+
+@contextlib.contextmanager
+def knobs(ctx, split=None, stage0=None):
+    try:
+        if split is not None:
+            ctx.set_split_budget(split)
+        if stage0 is not None:
+            ctx.set_stage0_budget(stage0)
+        yield
+    finally:
+        ctx.set_split_budget(DEFAULT_SPLIT)
+        ctx.set_stage0_budget(0)
+
+
+@pytest.mark.parametrize("split", [1, 16, 200])
+@pytest.mark.parametrize("name,n", [("bank_4x16_bugs", 20000), ("bank_6x24", 4000), ("ticket_2x10", 5000)])
+def test_split_generated(ctx, name, n, split):
+    hdr, ev, _ = gen.generate_config(name, 0, n)
+    with knobs(ctx, split=split):
+        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+
+
+@pytest.mark.parametrize("model", ["ticket", "bank"])
+def test_split_random_shapes(ctx, model):
+    """Both variants (<= 64 events / 8 pids and <= 128 events / 128 pids),
+    ill-formed, shared-pid and pending histories."""
+    rng = random.Random(77 if model == "ticket" else 78)
+    hs = []
+    for _ in range(3000):
+        n = rng.choice([4, 12, 20, 32, 40, 64, 90, 128])
+        if rng.random() < 0.5:
+            hs.append(histgen.random_history(rng, model, n, rng.randint(1, 12)))
+        else:
+            hs.append(histgen.wellformed_history(rng, model, n // 2, rng.randint(1, 12))[:n])
+    m = models.BY_NAME[model]
+    b = codec.encode(m, hs)
+    with knobs(ctx, split=8):
+        _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
+
+
+def test_split_after_refill(ctx):
+    hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 1000, 20000)
+    with knobs(ctx, split=64, stage0=8):
+        _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**7)
+
+
+def test_split_node_limits(ctx):
+    """max_nodes across the cut: BUDGET exactly where the single DFS stops."""
+    rng = random.Random(5)
+    hs = [histgen.random_history(rng, "ticket", 40, 1) for _ in range(400)]
+    hs += [histgen.random_history(rng, "ticket", 24, 2) for _ in range(400)]
+    b = codec.encode(models.TICKET, hs)
+    with knobs(ctx, split=2):
+        for budget in (3, 7, 100, 5000):
+            st, nd, _ = _compare(ctx, models.MODEL_TICKET, b.hdr, b.events, max_nodes=budget)
+            assert (nd <= budget).all()
+
+
+def test_split_early_exit(ctx):
+    hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 0, 8000)
+    st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr, ev, threads=8, max_nodes=10**7)
+    fails = np.nonzero((st_o == 0) | (st_o == 2))[0]
+    cut = int(fails[0])
+    with knobs(ctx, split=4):
+        st, nd, _, tot = ctx.check_arrays(models.MODEL_BANK, hdr, ev, max_nodes=10**7,
+                                          flags=EXH | device.QSMD_FLAG_EARLY_EXIT_BATCH)
+    assert np.array_equal(st[:cut + 1], st_o[:cut + 1]) and np.array_equal(nd[:cut + 1], nd_o[:cut + 1])
+    assert (st[cut + 1:] == codec.STATUS_SKIPPED).all()
+    assert tot["nodes"] == int(nd_o[:cut + 1].sum())
+
+
+def _heavy(name, n, k):
+    hdr, ev, _ = gen.generate_config(name, 0, n)
+    st, nd, _ = oracle_c.check_batch(gen.CONFIGS[name]["model_id"], hdr, ev, threads=8, max_nodes=10**7)
+    order = np.argsort(-nd.astype(np.int64))[:k]
+    return hdr, ev, order
+
+
+def _one(hdr, ev, i):
+    h = hdr[i:i + 1].copy()
+    a, n = int(h[0]["ev_off"]), int(h[0]["n_ev"])
+    h[0]["ev_off"] = 0
+    return h, ev[a:a + n].copy()
+
+
+@pytest.mark.parametrize("name", ["bank_4x16_bugs", "bank_6x24"])
+def test_split_api_single_history(ctx, name):
+    """qsmd_split_frontier + qsmd_check_tasks + qsmd_combine_tasks == the
+    single search, for any task count, and for tasks spread round-robin
+    over several callers (the multi-GPU split)."""
+    mid = gen.CONFIGS[name]["model_id"]
+    hdr, ev, order = _heavy(name, 4000, 12)
+    for i in order:
+        h, e = _one(hdr, ev, int(i))
+        st_o, nd_o, w_o = oracle_c.check_batch(mid, h, e, witness=True)
+        for min_tasks in (1, 16, 300):
+            fr, tasks, w_top = ctx.split_frontier(mid, h, e, min_tasks=min_tasks, witness=True)
+            assert fr.status in (0, 1, 2)
+            for ranks in (1, 3):
+                st = np.zeros(len(tasks), dtype=np.uint8)
+                nd = np.zeros(len(tasks), dtype=np.uint64)
+                wit = np.full((len(tasks), 64), 0xFF, dtype=np.uint8)
+                for r in range(ranks):
+                    sub = tasks[r::ranks]
+                    s, n_, w = ctx.check_tasks(mid, h, e, sub, witness=True)
+                    st[r::ranks], nd[r::ranks], wit[r::ranks] = s, n_, w
+                # tasks a caller skipped lie after one it found deciding
+                status, nodes, win = device.combine_tasks(fr, tasks, st, nd)
+                assert (status, nodes) == (int(st_o[0]), int(nd_o[0])), (i, min_tasks, ranks)
+                if status == codec.STATUS_LIN:
+                    path = wit[win] if win >= 0 else w_top
+                    d = int(np.argmax(np.append(path, 0xFF) == 0xFF))
+                    od = int(np.argmax(np.append(w_o, 0xFF) == 0xFF))
+                    assert d == od and np.array_equal(path[:d], w_o[:od])
+
+
+def test_split_api_edge_cases(ctx):
+    # empty history: decided above the cut (True, no tasks)
+    h = np.zeros(1, dtype=codec.HDR_DTYPE)
+    h[0] = (0, 0, 0, models.MODEL_BANK, 0, 0)
+    fr, tasks, _ = ctx.split_frontier(models.MODEL_BANK, h, np.zeros(0, dtype=codec.EV_DTYPE))
+    assert fr.status == codec.STATUS_LIN and len(tasks) == 0
+    # max_tasks smaller than the root's children: searched whole, no tasks
+    hdr, ev, order = _heavy("bank_4x16_bugs", 2000, 1)
+    h, e = _one(hdr, ev, int(order[0]))
+    st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, h, e)
+    fr, tasks, _ = ctx.split_frontier(models.MODEL_BANK, h, e, min_tasks=10**6, max_tasks=1)
+    status, nodes, _ = device.combine_tasks(fr, tasks, np.zeros(0, np.uint8), np.zeros(0, np.uint64))
+    assert (status, nodes) == (int(st_o[0]), int(nd_o[0]))
+    # node limit across the cut
+    fr, tasks, _ = ctx.split_frontier(models.MODEL_BANK, h, e, min_tasks=64, max_nodes=50)
+    st, nd, _ = ctx.check_tasks(models.MODEL_BANK, h, e, tasks, max_nodes=50)
+    st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, h, e, max_nodes=50)
+    assert device.combine_tasks(fr, tasks, st, nd, max_nodes=50)[:2] == (int(st_o[0]), int(nd_o[0]))
+
+
+@pytest.mark.parametrize("name", ["bank_4x16_bugs", "ticket_2x10"])
+def test_memo_verdicts(ctx, name):
+    hdr, ev, _ = gen.generate_config(name, 0, 20000)
+    mid = gen.CONFIGS[name]["model_id"]
+    st_o, nd_o, w_o = oracle_c.check_batch(mid, hdr, ev, threads=8, witness=True, max_nodes=10**7)
+    with knobs(ctx, split=16):
+        st, nd, w, tot = ctx.check_arrays(mid, hdr, ev, flags=EXH | MEMO, witness=True, max_nodes=10**7)
+    assert np.array_equal(st, st_o)
+    assert (nd <= nd_o).all()
+    for i in np.nonzero(st == codec.STATUS_LIN)[0]:
+        a, b = int(hdr[i]["ev_off"]), int(hdr[i]["ev_off"]) + int(hdr[i]["n_ev"])
+        assert np.array_equal(w[a:b], w_o[a:b]), i
+
+
+def test_adversarial_ticket_exhaustive_split(ctx):
+    """4 clients x 17 ops with one bug: 923201 reference nodes, searched by
+    the split stage with the exact count."""
+    h, e, _ = gen.adversarial_ticket(4, 17, bug=True)
+    st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_TICKET, h, e)
+    assert (int(st_o[0]), int(nd_o[0])) == (codec.STATUS_NONLIN, 923201)
+    st, nd, _, _ = ctx.check_arrays(models.MODEL_TICKET, h, e)
+    assert (int(st[0]), int(nd[0])) == (codec.STATUS_NONLIN, 923201)
+
+
+@pytest.mark.parametrize("bug", [True, False])
+def test_adversarial_ticket_memo(ctx, bug):
+    """BASELINE config 4: 8 clients x 64 ops, shared pid, heavy overlap;
+    (8!)^7 paths without memo, a few hundred states with it."""
+    h, e, _ = gen.adversarial_ticket(8, 64, bug=bug)
+    st_o, _, w_o = oracle_c.check_batch(models.MODEL_TICKET, h, e, memo=True, witness=True)
+    st, nd, w, _ = ctx.check_arrays(models.MODEL_TICKET, h, e, flags=EXH | MEMO, witness=True)
+    assert int(st[0]) == int(st_o[0]) == (codec.STATUS_NONLIN if bug else codec.STATUS_LIN)
+    if not bug:
+        assert np.array_equal(w, w_o)

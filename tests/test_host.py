@@ -173,3 +173,47 @@ def test_replay_witness_accepts_oracle_witnesses_and_rejects_others():
             assert not replay_witness(m, hist, wit[:-1]) or len(wit) == 0
         checked += 1
     assert checked > 50
+
+
+def test_combine_tasks_host():
+    """qsmd_combine_tasks (host code of the C ABI): the reference count is
+    the nodes above the cut up to the deciding task + every earlier subtree."""
+    fr = device.Frontier(status=codec.STATUS_NONLIN, depth=2, top_nodes=10, n_tasks=3)
+    tasks = np.zeros(3, dtype=device.TASK_DTYPE)
+    tasks["top_before"] = [3, 5, 8]
+    nodes = np.array([4, 2, 7], dtype=np.uint64)
+    # second subtree holds a linearisation
+    assert device.combine_tasks(fr, tasks, np.array([0, 1, 0], np.uint8), nodes) == (1, 5 + 4 + 2, 1)
+    # none does: exhausted above the cut
+    assert device.combine_tasks(fr, tasks, np.array([0, 0, 0], np.uint8), nodes) == (0, 10 + 13, -1)
+    # Map.! in the first subtree
+    assert device.combine_tasks(fr, tasks, np.array([2, 1, 0], np.uint8), nodes) == (2, 3 + 4, 0)
+    # node limit: the second subtree would cross it
+    assert device.combine_tasks(fr, tasks, np.array([0, 1, 0], np.uint8), nodes, max_nodes=10) == (4, 10, -1)
+    assert device.combine_tasks(fr, tasks, np.array([0, 1, 0], np.uint8), nodes, max_nodes=11) == (1, 11, 1)
+    # decided above the cut after the tasks (True at top node 9)
+    fr2 = device.Frontier(status=codec.STATUS_LIN, depth=2, top_nodes=9, n_tasks=3)
+    assert device.combine_tasks(fr2, tasks, np.array([0, 0, 0], np.uint8), nodes) == (1, 9 + 13, -1)
+    # a skipped task before any decision: skipped (batch early exit)
+    assert device.combine_tasks(fr, tasks, np.array([0, 5, 0], np.uint8), nodes)[0] == 5
+
+
+def test_oracle_memo_verdicts():
+    """The oracle's QSMD_FLAG_MEMO restatement keeps every verdict and never
+    counts more nodes; on the adversarial TicketDispenser history it turns
+    923201 nodes into a few dozen."""
+    for name in ("bank_4x16_bugs", "ticket_2x10", "bank_6x24"):
+        hdr, ev, _ = gen.generate_config(name, 0, 2000)
+        mid = gen.CONFIGS[name]["model_id"]
+        s1, n1, w1 = oracle_c.check_batch(mid, hdr, ev, threads=4, witness=True)
+        s2, n2, w2 = oracle_c.check_batch(mid, hdr, ev, threads=4, witness=True, memo=True)
+        assert np.array_equal(s1, s2) and (n2 <= n1).all()
+        assert np.array_equal(w1, w2)
+    h, e, _ = gen.adversarial_ticket(4, 17, bug=True)
+    assert oracle_c.check_batch(1, h, e)[1][0] == 923201
+    st, nd, _ = oracle_c.check_batch(1, h, e, memo=True)
+    assert st[0] == codec.STATUS_NONLIN and nd[0] < 100
+    for bug in (True, False):
+        h, e, _ = gen.adversarial_ticket(8, 64, bug=bug)
+        st, _, _ = oracle_c.check_batch(1, h, e, memo=True)
+        assert st[0] == (codec.STATUS_NONLIN if bug else codec.STATUS_LIN)
