@@ -494,7 +494,12 @@ __global__ __launch_bounds__(LANES) void frontier_search(SplitArgs p, uint32_t v
         top_search(d, s, a, lane, cut, limit, g, 0, nullptr, count, t0);
         if (count <= p.max_tasks) {
             first = atomicAdd(&p.task_count[variant], count);
-            if ((uint64_t)first + count > p.task_cap) first = ~0u;
+            if ((uint64_t)first + count > p.task_cap) {
+                // out of task slots: mark the part of the range below the cap as holes
+                for (uint64_t q = first; q < p.task_cap && q < (uint64_t)first + count; ++q)
+                    region[q].hist = ~0u;
+                first = ~0u;
+            }
         }
         int st;
         if (first != ~0u) {
@@ -559,7 +564,7 @@ __global__ __launch_bounds__(LANES) void task_search(SplitArgs p, uint32_t varia
             if (first + want >= count) exhausted = true;
             if (!busy) {
                 idx = first + sp_lane_prefix(idle);
-                if (idx < count) {
+                if (idx < count && tasks[idx].hist != ~0u) {   // ~0u: a hole (frontier overflow)
                     const qsmd_task T = tasks[idx];   // path bytes re-read below (no scratch)
                     g = T.hist;
                     const GiantRec* G = p.giants + g;

@@ -79,3 +79,87 @@ def device_checker(ctx, max_nodes=0):
         st, nd, _, _ = ctx.check_arrays(model_id, hdr, events, max_nodes=max_nodes)
         return st, nd
     return run
+
+
+# --------------------------------------------------------------------------
+# One very large history across ranks (BASELINE config 4).
+
+_NO_TASK = np.iinfo(np.int64).max
+
+
+def _allreduce(arr, op, group=None):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.int64))
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(t, op=op, group=group)
+    return t.numpy().astype(np.int64)
+
+
+def check_single_split(checker, model_id, hdr, events, rank, world, model0=None, flags=1,
+                       max_nodes=0, tasks_per_rank=64, round_tasks=None, group=None):
+    """Search ONE history with every rank.
+
+    Each rank cuts the search at the same frontier (checker.split_frontier
+    is deterministic), so no task list is exchanged; rank r searches the
+    tasks t = r, r + world, ... (round-robin in DFS order).  Work goes in
+    rounds over windows of the task list; after each round one MIN
+    all-reduce publishes the first task found deciding (True or Map.!), and
+    no rank searches a task after it -- every task before it has been
+    searched in full by its owner, so the node count stays exact.  Then one
+    SUM all-reduce gathers the per-task results (each rank contributes only
+    its own entries) and every rank folds them in DFS order.
+
+    checker: qsmd.device.Context (or anything with split_frontier /
+    check_tasks).  Returns (status, nodes, witness path or None, info dict).
+    """
+    import torch.distributed as dist
+
+    from . import device
+
+    fr, tasks, w_top = checker.split_frontier(model_id, hdr, events, model0, flags, max_nodes,
+                                              min_tasks=world * tasks_per_rank,
+                                              max_tasks=max(4096, 2 * world * tasks_per_rank),
+                                              witness=True)
+    n = len(tasks)
+    st_local = np.zeros(n, dtype=np.int64)           # status + 1 where searched here
+    nd_local = np.zeros(n, dtype=np.int64)
+    rows = {}
+    window = round_tasks or max(world, n)
+    best = _NO_TASK
+    rounds = 0
+    for c0 in range(0, n, window):
+        sel = np.arange(c0 + rank, min(c0 + window, n), world)
+        sel = sel[sel < best]
+        if len(sel):
+            s, nd, w = checker.check_tasks(model_id, hdr, events, tasks[sel], model0, flags, max_nodes,
+                                           witness=True)
+            st_local[sel] = s.astype(np.int64) + 1
+            nd_local[sel] = nd.astype(np.int64)
+            dec = sel[(s == 1) | (s == 2)]
+            for t in sel[s == 1]:
+                rows[int(t)] = w[int(np.nonzero(sel == t)[0][0])]
+            if len(dec):
+                best = min(best, int(dec.min()))
+        best = int(_allreduce(np.array([best]), dist.ReduceOp.MIN, group)[0])
+        rounds += 1
+        if best != _NO_TASK:
+            break
+    st_all = _allreduce(st_local, dist.ReduceOp.SUM, group)
+    nd_all = _allreduce(nd_local, dist.ReduceOp.SUM, group)
+    status = np.where(st_all > 0, st_all - 1, 5).astype(np.uint8)     # unsearched: SKIPPED
+    st_f, nodes, win = device.combine_tasks(fr, tasks, status, nd_all.astype(np.uint64), max_nodes)
+    witness = None
+    if st_f == 1:
+        if win >= 0:
+            mine = rows[win].astype(np.int64) + 1 if win in rows else np.zeros(64, dtype=np.int64)
+            row = _allreduce(mine, dist.ReduceOp.SUM, group) - 1
+            end = np.nonzero(row == 0xFF)[0]
+            witness = row[: int(end[0]) if len(end) else 64].astype(np.uint8)
+        else:
+            end = np.nonzero(w_top == 0xFF)[0]
+            witness = w_top[: int(end[0]) if len(end) else len(w_top)]
+    info = dict(n_tasks=n, depth=int(fr.depth), top_nodes=int(fr.top_nodes), rounds=rounds,
+                searched_here=int((st_local > 0).sum()), winner=win)
+    return st_f, nodes, witness, info

@@ -86,3 +86,92 @@ def test_two_rank_gloo_equals_single_process(config):
     cat_nd = np.array(results[0][6] + results[1][6])
     assert np.array_equal(cat_st, st) and np.array_equal(cat_nd, nd.astype(np.int64))
     assert results[0][2] == int((st == 0).any() or (st == 2).any())
+
+
+# ---------------------------------------------------------------------------
+# One history split across ranks: frontier in DFS order,
+# round-robin tasks, MIN all-reduce of the first deciding task, SUM gather,
+# ordered fold (qsmd_combine_tasks of the C ABI, host code).
+
+def _heavy_histories(k=6):
+    import oracle_c
+    from qsmd import gen
+    out = []
+    for name in ("bank_4x16_bugs", "ticket_2x10"):
+        hdr, ev, _ = gen.generate_config(name, 0, 600)
+        mid = gen.CONFIGS[name]["model_id"]
+        st, nd, _ = oracle_c.check_batch(mid, hdr, ev, threads=4)
+        for i in np.argsort(-nd.astype(np.int64))[:k]:
+            h = hdr[i:i + 1].copy()
+            a, n = int(h[0]["ev_off"]), int(h[0]["n_ev"])
+            h[0]["ev_off"] = 0
+            out.append((mid, h, ev[a:a + n].copy()))
+    return out
+
+
+def test_split_emulator_and_combine_equal_single_search():
+    """Frontier + independent subtree searches + the library's ordered fold
+    reproduce the single DFS exactly, for every cut depth."""
+    import oracle_c
+    import split_emu
+    from qsmd import device
+    emu = split_emu.EmuChecker()
+    for mid, h, e in _heavy_histories():
+        st_o, nd_o, w_o = oracle_c.check_batch(mid, h, e, witness=True)
+        for min_tasks in (1, 5, 40):
+            fr, tasks, w_top = emu.split_frontier(mid, h, e, min_tasks=min_tasks)
+            st, nd, wit = emu.check_tasks(mid, h, e, tasks)
+            status, nodes, win = device.combine_tasks(fr, tasks, st, nd)
+            assert (status, nodes) == (int(st_o[0]), int(nd_o[0]))
+            if status == 1:
+                path = wit[win] if win >= 0 else w_top
+                n = int(np.argmax(np.append(path, 0xFF) == 0xFF))
+                assert np.array_equal(path[:n], w_o[:n])
+
+
+def _split_worker(rank, world, port, round_tasks, out_q):
+    sys.path[:0] = [os.path.join(HERE, "..", "quickcheck-state-machine-distributed_amd"),
+                    os.path.join(HERE, "..", "oracle"), HERE]
+    import torch.distributed as dist
+
+    import split_emu
+    from qsmd import dist as qdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = []
+        for mid, h, e in _heavy_histories(3):
+            st, nodes, w, info = qdist.check_single_split(split_emu.EmuChecker(), mid, h, e, rank, world,
+                                                          tasks_per_rank=8, round_tasks=round_tasks)
+            res.append((int(st), int(nodes), None if w is None else [int(x) for x in w],
+                        info["searched_here"]))
+        out_q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("round_tasks", [4, None])
+def test_two_rank_gloo_single_history_split(round_tasks):
+    import oracle_c
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, round_tasks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for j, (mid, h, e) in enumerate(_heavy_histories(3)):
+        st_o, nd_o, w_o = oracle_c.check_batch(mid, h, e, witness=True)
+        for r in range(world):
+            st, nodes, w, _ = results[r][j]
+            assert (st, nodes) == (int(st_o[0]), int(nd_o[0]))
+            if st == 1:
+                assert w == [int(x) for x in w_o[:len(w)]] and (len(w) == len(w_o) or w_o[len(w)] == 0xFF)
+        if int(nd_o[0]) > 1000:          # split into tasks, and the ranks shared them
+            assert results[0][j][3] > 0 and results[1][j][3] > 0
