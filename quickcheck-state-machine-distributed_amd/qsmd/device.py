@@ -85,6 +85,8 @@ def combine_tasks(frontier, tasks, status, nodes, max_nodes=0):
     nodes = np.ascontiguousarray(nodes, dtype=np.uint64)
     st, nd, win = ctypes.c_uint8(), ctypes.c_uint64(), ctypes.c_int64()
     n = len(tasks)
+    if len(status) != n or len(nodes) != n:
+        raise ValueError("one status and one node count per task")
     rc = lib.qsmd_combine_tasks(ctypes.byref(frontier), _ptr(tasks) if n else None,
                                 _ptr(status) if n else None, _ptr(nodes) if n else None, n,
                                 int(max_nodes), ctypes.byref(st), ctypes.byref(nd), ctypes.byref(win))

@@ -93,8 +93,10 @@ def _allreduce(arr, op, group=None):
 
     t = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.int64))
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if dist.get_backend(group) == "nccl":          # RCCL: device tensors
+            t = t.to(torch.device("cuda", torch.cuda.current_device()))
         dist.all_reduce(t, op=op, group=group)
-    return t.numpy().astype(np.int64)
+    return t.cpu().numpy().astype(np.int64)
 
 
 def check_single_split(checker, model_id, hdr, events, rank, world, model0=None, flags=1,

@@ -9,6 +9,7 @@ exhaustive ones.
 """
 
 import contextlib
+import ctypes
 import random
 
 import numpy as np
@@ -147,13 +148,30 @@ def test_split_api_edge_cases(ctx):
     h[0] = (0, 0, 0, models.MODEL_BANK, 0, 0)
     fr, tasks, _ = ctx.split_frontier(models.MODEL_BANK, h, np.zeros(0, dtype=codec.EV_DTYPE))
     assert fr.status == codec.STATUS_LIN and len(tasks) == 0
-    # max_tasks smaller than the root's children: searched whole, no tasks
+    # max_tasks = 1: the deepest cut with a single task (or, when even the
+    # root has more children, the whole search done by the frontier itself)
     hdr, ev, order = _heavy("bank_4x16_bugs", 2000, 1)
     h, e = _one(hdr, ev, int(order[0]))
     st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, h, e)
-    fr, tasks, _ = ctx.split_frontier(models.MODEL_BANK, h, e, min_tasks=10**6, max_tasks=1)
-    status, nodes, _ = device.combine_tasks(fr, tasks, np.zeros(0, np.uint8), np.zeros(0, np.uint64))
-    assert (status, nodes) == (int(st_o[0]), int(nd_o[0]))
+    for m0 in (None, models.BankModel(0b1111, 0, (ctypes.c_int64 * 8)(5, 5, 5, 5, 0, 0, 0, 0))):
+        st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, h, e, m0)
+        fr, tasks, _ = ctx.split_frontier(models.MODEL_BANK, h, e, m0, min_tasks=10**6, max_tasks=1)
+        assert len(tasks) <= 1
+        st, nd, _ = ctx.check_tasks(models.MODEL_BANK, h, e, tasks, m0)
+        assert device.combine_tasks(fr, tasks, st, nd)[:2] == (int(st_o[0]), int(nd_o[0]))
+    rng = random.Random(11)
+    fallback = 0
+    for _ in range(200):
+        hist = histgen.random_history(rng, "bank", rng.randint(6, 30), rng.randint(2, 5))
+        b = codec.encode(models.BANK, [hist])
+        if b.encode_errors:
+            continue
+        st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, b.hdr, b.events)
+        fr, tasks, _ = ctx.split_frontier(models.MODEL_BANK, b.hdr, b.events, min_tasks=8, max_tasks=1)
+        fallback += fr.n_tasks == 0 and fr.depth == 0
+        st, nd, _ = ctx.check_tasks(models.MODEL_BANK, b.hdr, b.events, tasks)
+        assert device.combine_tasks(fr, tasks, st, nd)[:2] == (int(st_o[0]), int(nd_o[0]))
+    assert fallback > 0
     # node limit across the cut
     fr, tasks, _ = ctx.split_frontier(models.MODEL_BANK, h, e, min_tasks=64, max_nodes=50)
     st, nd, _ = ctx.check_tasks(models.MODEL_BANK, h, e, tasks, max_nodes=50)
