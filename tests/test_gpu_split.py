@@ -159,10 +159,14 @@ def test_split_api_edge_cases(ctx):
         assert len(tasks) <= 1
         st, nd, _ = ctx.check_tasks(models.MODEL_BANK, h, e, tasks, m0)
         assert device.combine_tasks(fr, tasks, st, nd)[:2] == (int(st_o[0]), int(nd_o[0]))
+    from kats import L, R
     rng = random.Random(11)
     fallback = 0
-    for _ in range(200):
-        hist = histgen.random_history(rng, "bank", rng.randint(6, 30), rng.randint(2, 5))
+    # three concurrent OpenAccounts at the root: more root children than max_tasks
+    opens = [(p, L(("OpenAccount", p))) for p in "abc"] + [(p, R("AccountCreated")) for p in "abc"]
+    hists = [opens, opens + [("a", L(("CheckBalance", "a"))), ("a", R(("Balance", 1)))]]
+    hists += [histgen.random_history(rng, "bank", rng.randint(6, 30), rng.randint(2, 5)) for _ in range(200)]
+    for hist in hists:
         b = codec.encode(models.BANK, [hist])
         if b.encode_errors:
             continue
