@@ -82,8 +82,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="bank_4x16", choices=sorted(gen.CONFIGS))
     ap.add_argument("--n-hist", type=int, default=1_000_000, help="histories per GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--split-budget", type=int, default=None,
+                    help="per-lane node budget before the split stage (library default if unset)")
+    ap.add_argument("--stage0-budget", type=int, default=None)
+    ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC summary written by profiles/profile.sh (for roofline.traffic)")
     args = ap.parse_args()
@@ -104,6 +108,11 @@ def main():
     log(f"[rank {rank}] generated {n} histories in {time.perf_counter() - t:.1f}s")
 
     ctx = device.Context(local)
+    if args.split_budget is not None:
+        ctx.set_split_budget(args.split_budget)
+    if args.stage0_budget is not None:
+        ctx.set_stage0_budget(args.stage0_budget)
+    flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
     d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
     d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
     d_st = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -113,7 +122,7 @@ def main():
 
     def step():
         ctx.check_device(model_id, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st.data_ptr(),
-                         d_nd.data_ptr(), None, d_tot.data_ptr(), stream=stream.cuda_stream)
+                         d_nd.data_ptr(), None, d_tot.data_ptr(), flags=flags, stream=stream.cuda_stream)
         if world > 1:
             dist.all_reduce(d_tot, op=dist.ReduceOp.SUM)
 
@@ -166,7 +175,7 @@ def main():
         "config": {"workload": args.config, "histories_per_gpu": n,
                    "clients": cfg["n_clients"], "ops": cfg["n_ops"],
                    "events_per_history": 2 * cfg["n_ops"], "parallelism": f"shard{world}",
-                   "mode": "exhaustive"},
+                   "mode": "memo" if args.memo else "exhaustive"},
         "nodes_per_sec": nodes_total * args.steps / elapsed,
         "verdicts": {"checked": int(tot[0]), "linearisable": int(tot[1]),
                      "nonlinearisable": int(tot[2]), "model_errors": int(tot[3]),
