@@ -200,6 +200,17 @@ int qsmd_set_stage0_grid(qsmd_ctx* ctx, uint64_t max_blocks);
  * search does not hold 63 idle lanes.  0 disables.  Results are unchanged. */
 int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
 
+/* Tuning knobs by name (none changes a result):
+ *   "stage0_persistent_grid"  > 0: the first stage runs as persistent
+ *                             wavefronts whose lanes each pull the next
+ *                             history as soon as they finish (this many
+ *                             workgroups); 0 (default): 64 histories per
+ *                             wavefront, staged together
+ *   "refill_min"              idle lanes before a persistent wavefront
+ *                             refills (1..64, default 8)
+ *   "split_budget", "stage0_budget", "stage0_grid"  as the setters below */
+int qsmd_set_param(qsmd_ctx* ctx, const char* name, uint64_t value);
+
 /* Tuning knob: node budget of the per-lane searches (default 4096).  A
  * history whose search needs more nodes is handed to the split stage, which
  * searches it again with many lanes (see "Split search" below).  0 disables

@@ -40,6 +40,8 @@ struct qsmd_ctx {
     unsigned long long* stamps = nullptr;   // diagnostic: stage-0 phase timings
     uint64_t stage0_budget = 0;        // stage-0 node budget before the refill stage (0 = none)
     uint64_t split_budget = 4096;      // per-lane node budget before the split stage (0 = none)
+    uint64_t stage0_persistent = 0;    // > 0: stage 0 = persistent refill_search (direct) with this grid
+    uint64_t refill_min = 8;           // refill kernels: idle lanes before a wavefront refills
     // QSMD_FLAG_MEMO table (device), allocated on first use
     unsigned long long* memo = nullptr;
     uint64_t memo_entries = 1ull << 22;
@@ -181,6 +183,28 @@ int qsmd_set_stage0_budget(qsmd_ctx* c, uint64_t nodes) {
     return QSMD_OK;
 }
 
+int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
+    if (!c || !name) return QSMD_ERR_ARG;
+    const std::string n(name);
+    if (n == "stage0_persistent_grid") {
+        if (value > 0x7FFFFFFFull) return fail(c, QSMD_ERR_ARG, "grid too large");
+        c->stage0_persistent = value;
+    } else if (n == "refill_min") {
+        if (value < 1 || value > 64) return fail(c, QSMD_ERR_ARG, "refill_min in 1..64");
+        c->refill_min = value;
+    } else if (n == "split_budget") {
+        c->split_budget = value;
+    } else if (n == "stage0_budget") {
+        c->stage0_budget = value;
+    } else if (n == "stage0_grid") {
+        if (value == 0 || value > 0x7FFFFFFFull) return fail(c, QSMD_ERR_ARG, "bad grid");
+        c->stage0_max_grid = value;
+    } else {
+        return fail(c, QSMD_ERR_ARG, "unknown parameter");
+    }
+    return QSMD_OK;
+}
+
 int qsmd_set_split_budget(qsmd_ctx* c, uint64_t nodes) {
     if (!c) return QSMD_ERR_ARG;
     c->split_budget = nodes;
@@ -238,8 +262,10 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
 
     // ---- workspace: defer lists, counters, partials, internal totals
-    const uint64_t g0 = std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), c->stage0_max_grid);
-    const uint64_t g0b = c->stage0_budget ? kRefillGrid : 0;   // no refill stage without a budget
+    const bool persistent = c->stage0_persistent != 0;
+    const uint64_t g0 = persistent ? c->stage0_persistent
+                                   : std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), c->stage0_max_grid);
+    const uint64_t g0b = c->stage0_budget && !persistent ? kRefillGrid : 0;   // no refill stage without a budget
     const uint64_t gfx = early ? std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), 4096) : 0;
     const bool split = c->split_budget && (!max_nodes || c->split_budget < max_nodes);
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
@@ -290,6 +316,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a.nodes = nodes;
     a.witness = (flags & QSMD_FLAG_WITNESS) ? witness : nullptr;
     a.timed_out = cnt + 2;
+    a.refill_min = (uint32_t)c->refill_min;
     uint32_t* lg = reinterpret_cast<uint32_t*>(c->ws + off_lg);
     if (split) {
         a.giant_list = lg;
@@ -316,7 +343,17 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         a0.heavy_count = cnt + 7;
         a0.stage0_budget = c->split_budget;
     }
-    HIP_TRY(c, launch_compact(a0, (uint32_t)g0, s), "stage 0 launch");
+    if (persistent) {                   // persistent lanes, each refilled with its own history
+        SearchArgs ad = a;
+        ad.list = nullptr;
+        ad.defer_list = l0;
+        ad.defer_count = cnt + 0;
+        ad.queue_head = cnt + 12;
+        ad.partials = part;
+        HIP_TRY(c, launch_refill(ad, (uint32_t)g0, s), "stage 0 (persistent) launch");
+    } else {
+        HIP_TRY(c, launch_compact(a0, (uint32_t)g0, s), "stage 0 launch");
+    }
     HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
     // stage 0b: histories over the stage-0 node budget, persistent refill
     SearchArgs ab = a;

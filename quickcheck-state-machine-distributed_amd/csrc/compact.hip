@@ -588,15 +588,21 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
 // a.list, head counter a.queue_head).  Idle lanes refill together once at
 // least kRefillMin of them are idle (or no lane is busy), with one atomic per
 // wavefront; each refilled lane stages its history into its own LDS column.
+//
+// Direct mode (a.list == null): the same loop over histories 0 .. n_hist-1 as
+// a persistent replacement of compact_search; each refilled lane validates
+// and stages its own history (deferring the ones stage 0 cannot hold), so a
+// lane never waits for the slowest lane of a 64-history group.
 template <uint32_t MODEL>
 __global__ __launch_bounds__(C_LANES) void refill_search(SearchArgs a) {
     constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
-    constexpr uint32_t kRefillMin = 8;
     __shared__ uint32_t s_ev[C_MAXEV][C_LANES];
     __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
 
     const int lane = threadIdx.x;
-    const uint32_t count = *a.list_count;
+    const bool direct = a.list == nullptr;
+    const uint32_t kRefillMin = a.refill_min ? a.refill_min : 8u;
+    const uint32_t count = direct ? (uint32_t)a.n_hist : *a.list_count;
     Counters cnt;
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t limit = stage_limit(a);
@@ -617,15 +623,31 @@ __global__ __launch_bounds__(C_LANES) void refill_search(SearchArgs a) {
             if (first + want >= count) exhausted = true;
             if (!busy) {
                 const uint32_t idx = first + lane_prefix(idle);
-                if (idx < count && !beyond_first_fail(a, a.list[idx])) {   // else: early_exit_fixup
-                    h = a.list[idx];
+                const uint32_t hh = idx < count ? (direct ? idx : a.list[idx]) : 0u;
+                if (idx < count && !beyond_first_fail(a, hh)) {   // else: early_exit_fixup
+                    h = hh;
                     const qsmd_hdr H = a.hdr[h];
                     n_ev = H.n_ev;
                     ev_off = H.ev_off;
+                    bool enc_ok = true, small = true;
+                    if (direct) {                             // stage 0's checks
+                        enc_ok = H.model_id == MODEL && n_ev <= QSMD_MAX_EVENTS && H.n_pid <= QSMD_MAX_PIDS &&
+                                 (uint64_t)ev_off + n_ev <= a.n_events;
+                        small = enc_ok && n_ev <= (uint32_t)C_MAXEV && H.n_pid <= 8u && a.m0_small;
+                    }
                     Staged s{0u, 0u, 0u, 0u, 0u, true, true};
-                    stage_lane<MODEL>(a, H, s_ev, lane, s);   // validated by stage 0
-                    dfs.init(s, a, s_bal, lane);
-                    busy = true;
+                    if (small) stage_lane<MODEL>(a, H, s_ev, lane, s);   // (list mode: validated by stage 0)
+                    if (enc_ok && (!small || (s.ok && !s.fits))) {
+                        a.defer_list[atomicAdd(a.defer_count, 1u)] = h;        // -> stage 1
+                    } else if (!enc_ok || !s.ok || n_ev == 0) {
+                        const int st = n_ev == 0 && enc_ok ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_ENCODE_ERROR;
+                        a.status[h] = (uint8_t)st;
+                        if (a.nodes) a.nodes[h] = 0;
+                        cnt.add(st, 0);
+                    } else {
+                        dfs.init(s, a, s_bal, lane);
+                        busy = true;
+                    }
                 }
             }
         }

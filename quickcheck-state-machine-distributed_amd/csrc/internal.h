@@ -30,6 +30,7 @@ struct SearchArgs {
     uint32_t* heavy_count;
     uint32_t* queue_head;
     uint64_t stage0_budget;
+    uint32_t refill_min;          // refill stage: idle lanes before a refill (0 = 8)
     uint32_t flags;
     uint32_t model_id;
     uint64_t max_nodes;           // 0 = unbounded

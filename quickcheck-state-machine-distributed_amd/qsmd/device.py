@@ -69,6 +69,7 @@ EXPORTS = {
     "qsmd_timing_reset": (_I, [_P]),
     "qsmd_timing_read": (_I, [_P, _P, _P, _U64, ctypes.POINTER(_U64)]),
     "qsmd_set_split_budget": (_I, [_P, _U64]),
+    "qsmd_set_param": (_I, [_P, ctypes.c_char_p, _U64]),
     "qsmd_set_memo_capacity": (_I, [_P, _U64]),
     "qsmd_split_frontier": (_I, [_P, _U32, _P, _P, _U64, _P, _U32, _U64, _U32, _P, _U64, _P, _P]),
     "qsmd_check_tasks": (_I, [_P, _U32, _P, _P, _U64, _P, _U32, _U64, _P, _U64, _P, _P, _P]),
@@ -199,6 +200,9 @@ class Context:
 
     def set_stage0_grid(self, max_blocks):
         self._check(self._lib.qsmd_set_stage0_grid(self._h, int(max_blocks)), "qsmd_set_stage0_grid")
+
+    def set_param(self, name, value):
+        self._check(self._lib.qsmd_set_param(self._h, name.encode(), int(value)), f"qsmd_set_param({name})")
 
     def set_split_budget(self, nodes):
         self._check(self._lib.qsmd_set_split_budget(self._h, int(nodes)), "qsmd_set_split_budget")
