@@ -287,10 +287,11 @@ int qsmd_combine_tasks(const qsmd_frontier* frontier, const qsmd_task* tasks,
                        uint64_t max_nodes, uint8_t* status_out, uint64_t* nodes_out,
                        int64_t* winner_out);
 
-/* Diagnostic: when stamps_dev (device memory, 4 x u64 per stage-0
+/* Diagnostic: when stamps_dev (device memory, 8 x u64 per stage-0
  * workgroup) is non-NULL, stage 0 runs an instrumented build that records
  * per-workgroup s_memtime totals of its phases (staging, search, output,
- * groups processed).  NULL restores the production kernel. */
+ * groups processed) and its residency (s_memrealtime at start and end,
+ * HW_ID, XCC_ID).  NULL restores the production kernel. */
 int qsmd_diag_stamps(qsmd_ctx* ctx, void* stamps_dev);
 
 /* Device time (ms, HIP events on the launch stream) of the search kernels of

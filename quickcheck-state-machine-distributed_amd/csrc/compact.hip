@@ -482,7 +482,8 @@ struct Counters {
 // -------------------------------------------------------------- stage 0
 
 // STAMP = diagnostic build: lane 0 accumulates s_memtime deltas of the
-// phases (header+staging, search, output) into a.stamps[block][4].
+// phases (header+staging, search, output, groups) into a.stamps[block][0..3]
+// and records its residency (realtime start/end, HW_ID, XCC_ID) in [4..7].
 template <uint32_t MODEL, bool STAMP>
 __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
     constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
@@ -498,6 +499,7 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
     const bool tiered = a.stage0_budget < user_limit && a.heavy_list != nullptr;
     const uint64_t limit = tiered ? a.stage0_budget : user_limit;
     uint64_t st_acc[4] = {0, 0, 0, 0}, ts_a = 0, ts_b = 0;
+    const uint64_t rt0 = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
 
     for (uint64_t base = (uint64_t)blockIdx.x * C_LANES; base < total;
          base += (uint64_t)gridDim.x * C_LANES) {
@@ -576,7 +578,12 @@ __global__ __launch_bounds__(C_LANES) void compact_search(SearchArgs a) {
     if constexpr (STAMP) {
         if (lane == 0) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) a.stamps[(uint64_t)blockIdx.x * 4 + k] = st_acc[k];
+            for (int k = 0; k < 4; ++k) a.stamps[(uint64_t)blockIdx.x * 8 + k] = st_acc[k];
+            // residency: realtime (100 MHz) at start / end, HW_ID, XCC_ID
+            a.stamps[(uint64_t)blockIdx.x * 8 + 4] = rt0;
+            a.stamps[(uint64_t)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+            a.stamps[(uint64_t)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            a.stamps[(uint64_t)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
         }
     }
     cnt.flush(a.partials, lane);

@@ -57,7 +57,7 @@ def main():
         return
     # diagnostic build: per-phase s_memtime cycles per 64-history group
     g0 = min((args.n + 63) // 64, 65536)
-    st = torch.zeros(g0 * 4, dtype=torch.int64, device=dev)
+    st = torch.zeros(g0 * 8, dtype=torch.int64, device=dev)
     ctx.set_stage0_grid(65536)
     ctx.set_stage0_budget(0)
     ctx.diag_stamps(st.data_ptr())
@@ -66,7 +66,19 @@ def main():
                      d_st.data_ptr(), d_nd.data_ptr(), None, None, stream=stream)
     s0, _ = ctx.timing_read()
     ctx.diag_stamps(None)
-    stamps = st.view(g0, 4).cpu().numpy().astype(np.float64)
+    raw = st.view(g0, 8).cpu().numpy()
+    stamps = raw[:, :4].astype(np.float64)
+    # residency: waves resident per SIMD over the kernel (realtime 100 MHz)
+    t0, t1 = raw[:, 4], raw[:, 5]
+    hw, xcc = raw[:, 6], raw[:, 7]
+    simd = (xcc & 0xF) * 10**6 + ((hw >> 13) & 7) * 10**4 + ((hw >> 12) & 1) * 10**3 + \
+        ((hw >> 8) & 0xF) * 10 + ((hw >> 4) & 3)
+    span = float(t1.max() - t0.min())
+    n_simd = len(np.unique(simd))
+    resid = {"span_us": span / 100.0, "simds_seen": int(n_simd),
+             "mean_waves_per_simd": float((t1 - t0).sum() / span / max(n_simd, 1)),
+             "wave_life_us_p50_p90_max": [float(np.percentile(t1 - t0, q)) / 100.0 for q in (50, 90, 100)],
+             "start_spread_us": float(np.percentile(t0 - t0.min(), 99)) / 100.0}
     groups = stamps[:, 3].sum()
     nd = d_nd.cpu().numpy()
     diag = {"stamped_kernel_ms": float(s0[0]),
@@ -74,7 +86,7 @@ def main():
                                  "output": stamps[:, 2].sum() / groups},
             "search_cycles_p50_p90_max": [float(np.percentile(stamps[:, 1], q)) for q in (50, 90, 100)],
             "nodes_mean": float(nd.mean()), "nodes_group_max_mean": float(nd.reshape(-1, 64).max(1).mean())
-            if args.n % 64 == 0 else None}
+            if args.n % 64 == 0 else None, "residency": resid}
     print(json.dumps({"config": args.config, "n": args.n, "variants": out, "diag": diag}, indent=1))
 
 
