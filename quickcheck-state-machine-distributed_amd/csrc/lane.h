@@ -1,0 +1,499 @@
+// lane.h -- the per-lane search machinery shared by the compact-domain
+// kernels (csrc/compact.hip: stage 0 and the refill stage; csrc/spread.hip:
+// the dynamic split stage): the compressed event format, the staging paths,
+// and LaneDFS, the reference DFS (src/Linearisability.hs:25-69 over the
+// Lemma L1 event bitset) as a per-lane state machine for histories of at
+// most 32 events and 8 pids.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "internal.h"
+#include "models.h"
+
+namespace qsmd {
+
+namespace {
+
+
+constexpr int C_MAXEV = 32;
+constexpr int C_LANES = 64;
+constexpr int C_CHUNK = 16;
+constexpr int32_t V19_MIN = -(1 << 18), V19_MAX = (1 << 18) - 1;   // model0 values (api.hip m0_small)
+
+// compressed event (one u32 per event, LDS [event][lane]):
+//   invocation  pid 3 | 0 | code 3 | a 3 | b 3 | r 5 | val 14 (signed)
+//   response    pid 3 | 1 | code 3 | val 25 (signed)
+// r: in a paired history (every pid alternates invocation / response), the
+// index of the response paired with the invocation (0 = none: pending).
+// Staging writes a marker instead of an event it cannot hold: an invocation
+// with code 7 (not an encodable event: ENCODE_ERROR) or code 6 (a value
+// outside the ranges above: the history goes to stage 1).
+constexpr int32_t IVAL_BITS = 14, RVAL_BITS = 25;
+constexpr uint32_t MARK_BAD = 0x70u, MARK_WIDE = 0x60u;
+__device__ __forceinline__ uint32_t c_code(uint32_t w) { return (w >> 4) & 7u; }
+__device__ __forceinline__ uint32_t c_a(uint32_t w) { return (w >> 7) & 7u; }
+__device__ __forceinline__ uint32_t c_b(uint32_t w) { return (w >> 10) & 7u; }
+__device__ __forceinline__ uint32_t c_r(uint32_t w) { return (w >> 13) & 31u; }
+__device__ __forceinline__ int32_t c_ival(uint32_t w) { return (int32_t)w >> (32 - IVAL_BITS); }
+__device__ __forceinline__ int32_t c_rval(uint32_t w) { return (int32_t)w >> (32 - RVAL_BITS); }
+
+__device__ __forceinline__ uint32_t below32(uint32_t r) { return (uint32_t)((1ull << r) - 1ull); }
+
+// candidates: remaining invocations before the first remaining response
+// (takeInvocations, src/Linearisability.hs:25-28); branch-free
+__device__ __forceinline__ uint32_t cands(uint32_t rem, uint32_t INV, uint32_t RESP) {
+    const uint32_t R = (uint32_t)__builtin_ctzll((uint64_t)(rem & RESP) | (1ull << 32));
+    return rem & INV & below32(R);
+}
+
+// Expected Bank response constructor of `post` (test/Bank.hs:118-131) as a
+// table lookup, index = code*4 + ex_a*2 + ge (3 bits per entry):
+//   Open: ex_a ? AccountAlreadyExists : AccountCreated   Deposit: DepositMade
+//   Withdraw: ge ? WithdrawalMade : InsufficientFunds    CheckBalance: Balance
+//   Transfer: ge ? TransferMade : InsufficientFunds
+constexpr uint64_t bank_exp_table() {
+    uint64_t t = 0;
+    for (uint32_t code = 0; code < 5; ++code)
+        for (uint32_t exa = 0; exa < 2; ++exa)
+            for (uint32_t ge = 0; ge < 2; ++ge) {
+                uint32_t e = QSMD_BANK_INSUFFICIENT_FUNDS;
+                if (code == QSMD_BANK_OPEN_ACCOUNT) e = exa ? QSMD_BANK_ACCOUNT_ALREADY_EXISTS : QSMD_BANK_ACCOUNT_CREATED;
+                else if (code == QSMD_BANK_DEPOSIT) e = QSMD_BANK_DEPOSIT_MADE;
+                else if (code == QSMD_BANK_WITHDRAW) e = ge ? QSMD_BANK_WITHDRAWAL_MADE : QSMD_BANK_INSUFFICIENT_FUNDS;
+                else if (code == QSMD_BANK_CHECK_BALANCE) e = QSMD_BANK_BALANCE;
+                else e = ge ? QSMD_BANK_TRANSFER_MADE : QSMD_BANK_INSUFFICIENT_FUNDS;
+                t |= (uint64_t)e << (3 * (code * 4 + exa * 2 + ge));
+            }
+    return t;
+}
+constexpr uint64_t kBankExp = bank_exp_table();
+// per request code: sign of the step on account a (Deposit +1, Withdraw and
+// Transfer -1, Open / CheckBalance 0); an absent account is created with the
+// money exactly when the sign is non-zero (insertWith, test/Bank.hs:96-97)
+constexpr uint32_t kBankNeg = (1u << QSMD_BANK_WITHDRAW) | (1u << QSMD_BANK_TRANSFER);
+constexpr uint32_t kBankPos = (1u << QSMD_BANK_DEPOSIT);
+
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// include/qsmd.h encoding rules, branch-free (the pid range is checked
+// against the header's n_pid by finish_lane).
+template <uint32_t MODEL>
+__device__ __forceinline__ bool valid_bits(uint32_t lo) {
+    const uint32_t c = (lo >> 8) & 0xFFu, ea = (lo >> 16) & 0xFFu, eb = lo >> 24;
+    const bool pid_ok = (lo & 0x78u) == 0u;                 // pid < 8
+    if constexpr (MODEL == QSMD_MODEL_TICKET) {
+        return pid_ok & (c <= 1u);
+    } else {
+        const bool resp = (lo & 0x80u) != 0u;
+        const bool inv_ok = (c <= QSMD_BANK_TRANSFER) & (ea < 8u) & ((c != QSMD_BANK_TRANSFER) | (eb < 8u));
+        return pid_ok & (resp ? (c <= QSMD_BANK_BALANCE) : inv_ok);
+    }
+}
+
+// The compressed word of one event, or a marker (MARK_BAD / MARK_WIDE).
+template <uint32_t MODEL>
+__device__ __forceinline__ uint32_t compress(uint32_t lo, int32_t val) {
+    const bool resp = (lo & 0x80u) != 0u;
+    const uint32_t head = (lo & 7u) | ((lo >> 4) & 8u) | ((lo >> 4) & 0x70u);   // pid | resp | code
+    const uint32_t inv = head | ((lo >> 9) & 0x380u) | ((lo >> 14) & 0x1C00u) | ((uint32_t)val << (32 - IVAL_BITS));
+    const uint32_t rsp = head | ((uint32_t)val << (32 - RVAL_BITS));
+    const int32_t half = resp ? (1 << (RVAL_BITS - 1)) : (1 << (IVAL_BITS - 1));
+    const bool fit = (uint32_t)(val + half) < (uint32_t)(2 * half);
+    const uint32_t w = resp ? rsp : inv;
+    return !valid_bits<MODEL>(lo) ? MARK_BAD : (fit ? w : MARK_WIDE);
+}
+
+// The DFS stack: 16 levels x 8 bits in 4 VGPRs.  Selection goes through an
+// empty asm so hipcc keeps it a register select (it otherwise turns the
+// select tree into a scratch-memory indexed load).
+struct Stack16 {
+    uint32_t w[4];
+    __device__ __forceinline__ uint32_t word(uint32_t d) const {
+        uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3];
+        asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+        const uint32_t k = d >> 2;
+        const uint32_t lo = (k & 1u) ? x1 : x0, hi = (k & 1u) ? x3 : x2;
+        return (k & 2u) ? hi : lo;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t d) const {
+        return (word(d) >> ((d & 3u) * 8u)) & 0xFFu;
+    }
+    __device__ __forceinline__ void put(uint32_t d, uint32_t v) {
+        const uint32_t k = d >> 2, sh = (d & 3u) * 8u;
+        const uint32_t keep = ~(0xFFu << sh), ins = v << sh;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) w[q] = (q == k) ? ((w[q] & keep) | ins) : w[q];
+    }
+};
+
+struct Staged {
+    uint32_t INV, RESP, P0, P1, P2;
+    bool ok, fits, paired;
+};
+
+// One lane stages its own history: C_CHUNK loads in flight (index clamped
+// into the history, no exec-masked branches), compress into its LDS column.
+template <uint32_t MODEL>
+__device__ __forceinline__ void stage_lane(const SearchArgs& a, const qsmd_hdr& H, uint32_t (*s_ev)[C_LANES],
+                                           int lane) {
+    const uint32_t n_ev = H.n_ev;
+    if (n_ev == 0) return;
+    const uint2* evp = a.events + H.ev_off;
+    const uint32_t last = n_ev - 1u;
+#pragma unroll 1
+    for (uint32_t c0 = 0; c0 < n_ev; c0 += C_CHUNK) {
+        uint2 x[C_CHUNK];
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)C_CHUNK; ++k) {
+            const uint32_t e = c0 + k;
+            x[k] = evp[e < last ? e : last];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)C_CHUNK; ++k)
+            if (c0 + k < n_ev) s_ev[c0 + k][lane] = compress<MODEL>(x[k].x, (int32_t)x[k].y);
+    }
+}
+
+// The whole wavefront stages 64 histories packed back to back with one
+// common length N0 starting at event off0: the 64*N0-event block is read
+// with fully coalesced 16-byte loads (a per-lane history walk touches 64
+// cache lines per wave instruction), each event is compressed and written
+// to its history's lane column.
+__device__ __forceinline__ uint32_t magic_div(uint32_t N0) { return (uint32_t)(0xFFFFFFFFull / N0) + 1u; }
+
+template <uint32_t MODEL>
+__device__ __forceinline__ void stage_packed(const SearchArgs& a, uint32_t N0, uint32_t off0,
+                                             uint32_t (*s_ev)[C_LANES], int lane) {
+    // history of block event g: exact for g < 2^16 (g * N0 < 2^21 << 2^32)
+    const uint32_t mg = magic_div(N0);
+    auto put = [&](uint32_t g, uint32_t lo, int32_t val) {
+        const uint32_t hh = __umulhi(g, mg);
+        s_ev[g - hh * N0][hh] = compress<MODEL>(lo, val);
+    };
+    const uint32_t total_ev = 64u * N0;
+    if ((off0 & 1u) == 0u) {
+        const uint4* blk = reinterpret_cast<const uint4*>(a.events + off0);
+        for (uint32_t k0 = 0; k0 < total_ev / 2u; k0 += 4u * 64u) {
+            uint4 x[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t q = k0 + u * 64u + (uint32_t)lane;
+                x[u] = q < total_ev / 2u ? blk[q] : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t q = k0 + u * 64u + (uint32_t)lane;
+                if (q < total_ev / 2u) {
+                    put(2u * q, x[u].x, (int32_t)x[u].y);
+                    put(2u * q + 1u, x[u].z, (int32_t)x[u].w);
+                }
+            }
+        }
+    } else {
+        const uint2* blk = a.events + off0;
+        for (uint32_t k0 = 0; k0 < total_ev; k0 += 8u * 64u) {
+            uint2 x[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                const uint32_t g = k0 + u * 64u + (uint32_t)lane;
+                x[u] = g < total_ev ? blk[g] : make_uint2(0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                const uint32_t g = k0 + u * 64u + (uint32_t)lane;
+                if (g < total_ev) put(g, x[u].x, (int32_t)x[u].y);
+            }
+        }
+    }
+}
+
+// Per lane, over its own column: the encoding checks (markers, pid <
+// n_pid), the register masks, and the pairing of every invocation with the
+// response of the same pid that follows it when every pid alternates
+// invocation / response (SURVEY.md §8a Lemma L1.4: in such a history the
+// only candidate of pid p is its first remaining invocation, and its
+// response is the next response of p, so the pair is static).  The pair
+// index is OR-ed into the invocation word (r field).
+__device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane, uint32_t n_ev, uint32_t n_pid,
+                                            Staged& s) {
+    uint32_t W[C_MAXEV];
+#pragma unroll
+    for (uint32_t e = 0; e < (uint32_t)C_MAXEV; ++e) W[e] = s_ev[e][lane];
+    uint32_t open = 0u, ps_lo = 0u, ps_hi = 0u, unpaired = 0u, bad = 0u, wide = 0u;
+#pragma unroll
+    for (uint32_t e = 0; e < (uint32_t)C_MAXEV; ++e) {
+        if (e >= n_ev) break;
+        const uint32_t w = W[e];
+        const uint32_t bit = 1u << e;
+        const uint32_t p = w & 7u, resp = (w >> 3) & 1u, mk = w & 0x78u;
+        bad |= ((mk == MARK_BAD) | (p >= n_pid)) ? 1u : 0u;
+        wide |= mk == MARK_WIDE ? 1u : 0u;
+        s.RESP |= resp ? bit : 0u;
+        s.INV |= resp ? 0u : bit;
+        s.P0 |= (w & 1u) ? bit : 0u;
+        s.P1 |= (w & 2u) ? bit : 0u;
+        s.P2 |= (w & 4u) ? bit : 0u;
+        // pairing: ps = event index of the open invocation per pid (8 bits each)
+        const uint32_t ob = (open >> p) & 1u, sh = (p & 3u) * 8u;
+        const bool hi = p >= 4u;
+        const uint32_t j = ((hi ? ps_hi : ps_lo) >> sh) & 31u;
+        unpaired |= resp ? (ob ^ 1u) : ob;
+        open ^= (resp ? ob : (ob ^ 1u)) << p;                 // inv opens, its resp closes
+        const uint32_t ins = (ps_lo & ~(0xFFu << sh)) | (e << sh), insh = (ps_hi & ~(0xFFu << sh)) | (e << sh);
+        ps_lo = (!resp && !hi) ? ins : ps_lo;
+        ps_hi = (!resp && hi) ? insh : ps_hi;
+        if (resp & ob) atomicOr(&s_ev[j][lane], e << 13);
+    }
+    s.ok = bad == 0u;
+    s.fits = wide == 0u;
+    s.paired = unpaired == 0u;
+}
+
+// --------------------------------------------------------------- the DFS
+
+// Per-lane search state (registers) over the history in LDS column `lane`.
+// step() runs one iteration: an optional backtrack followed by one
+// candidate try; it returns -1 to continue or the final QSMD_STATUS_*
+// (QSMD_STATUS_BUDGET = `limit` nodes reached before a decision).
+// MODE: M_GENERAL (any pid pattern: the response and the removed invocation
+// come from the bit-sliced pid masks), M_PAIRED (every history of the
+// wavefront is paired: the response index is read from the invocation word)
+// or M_LANE (per-lane `paired` flag).
+enum { M_GENERAL = 0, M_PAIRED = 1, M_LANE = 2 };
+
+template <uint32_t MODEL>
+struct LaneDFS {
+    static constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
+    uint32_t INV, RESP, P0, P1, P2, ALL;
+    uint32_t rem, cand, depth, ex, neg, RS, found;
+    uint32_t base;          // depth of the search root (0; the task depth in split_search)
+    bool paired;
+    uint64_t nodes;
+    Stack16 stk;
+
+    // events whose pid equals the pid of event j (bit-sliced compare)
+    __device__ __forceinline__ uint32_t same_pid(uint32_t j) const {
+        const uint32_t m0 = 0u - ((P0 >> j) & 1u), m1 = 0u - ((P1 >> j) & 1u), m2 = 0u - ((P2 >> j) & 1u);
+        return ~((P0 ^ m0) | (P1 ^ m1) | (P2 ^ m2)) & ALL;
+    }
+
+    __device__ __forceinline__ void init(const Staged& s, const SearchArgs& a, int32_t (*s_bal)[C_LANES],
+                                         int lane) {
+        INV = s.INV; RESP = s.RESP; P0 = s.P0; P1 = s.P1; P2 = s.P2;
+        ALL = INV | RESP;
+        rem = ALL;
+        cand = cands(rem, INV, RESP);
+        depth = 0; found = 0; nodes = 0; RS = 0; base = 0;
+        paired = s.paired;
+        stk.w[0] = stk.w[1] = stk.w[2] = stk.w[3] = 0u;
+        ex = a.m0_exists; neg = 0;
+        if constexpr (BANK) {
+#pragma unroll
+            for (int q = 0; q < QSMD_BANK_MAX_ACCOUNTS; ++q) {
+                const bool e = (ex >> q) & 1u;
+                const int32_t v = e ? (int32_t)a.m0_val[q] : 0;
+                s_bal[q][lane] = v;
+                neg |= (e && v < 0) ? (1u << q) : 0u;
+            }
+        }
+    }
+
+    // evc[e * STRIDE] = compressed event e (the lane's LDS column: STRIDE = 64;
+    // a history shared by the wavefront: STRIDE = 1)
+    template <int MODE>
+    __device__ __forceinline__ bool is_paired() const {
+        return MODE == M_PAIRED || (MODE == M_LANE && paired);
+    }
+
+    template <int STRIDE, int MODE = M_GENERAL>
+    __device__ __forceinline__ int step(const SearchArgs& a, const uint32_t* evc,
+                                        int32_t (*s_bal)[C_LANES], int lane, uint64_t limit) {
+        if (!cand) {
+            // no children: a leaf => True (any' []), the root => False (any []);
+            // a subtree rooted at depth base > 0 is an inner node of the reference tree
+            if (!found || depth == base)
+                return (!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE;
+            // ---- backtrack: restore the parent level exactly
+            --depth;
+            const uint32_t st = stk.get(depth);
+            const uint32_t j = st & 31u;
+            const uint32_t cj = (BANK || MODE != M_GENERAL) ? evc[j * STRIDE] : 0u;
+            if (is_paired<MODE>()) {
+                rem |= (1u << j) | (1u << c_r(cj));
+            } else {
+                const uint32_t gone = ~rem & same_pid(j);
+                rem |= (1u << (31 - __builtin_clz(gone & INV))) | (1u << (31 - __builtin_clz(gone & RESP)));
+            }
+            if constexpr (BANK) {
+                const uint32_t code = c_code(cj), ia = c_a(cj), ib = c_b(cj);
+                const int32_t m = c_ival(cj);
+                const uint32_t pa = (st >> 5) & 1u, pb = (st >> 6) & 1u;
+                const uint32_t tr = code == QSMD_BANK_TRANSFER ? 1u : 0u;
+                const int32_t ba = s_bal[ia][lane], bb = s_bal[ib][lane];
+                // undo Transfer's deposit on b, then the step on a
+                const int32_t rb = (pb | (ia == ib)) ? bb - m : 0;
+                const int32_t cur_a = (tr & (ia == ib)) ? rb : ba;
+                const int32_t sa = (int32_t)((kBankPos >> code) & 1u) - (int32_t)((kBankNeg >> code) & 1u);
+                const int32_t ra = pa ? cur_a - sa * m : 0;
+                const int32_t fb = tr ? rb : bb;
+                s_bal[ib][lane] = fb;                  // a no-op unless Transfer
+                s_bal[ia][lane] = ra;                  // written last (ia == ib)
+                ex = (ex & ~((1u << ia) | (tr << ib))) | (pa << ia) | ((tr & pb) << ib);
+                const int32_t vb = ia == ib ? ra : fb;
+                neg &= ~((1u << ia) | (1u << ib));
+                neg |= ((ra < 0) ? ((ex >> ia) & 1u) : 0u) << ia;
+                neg |= ((vb < 0) ? ((ex >> ib) & 1u) : 0u) << ib;
+            } else {
+                RS &= ~(1u << depth);
+            }
+            cand = cands(rem, INV, RESP) & ~below32(j + 1u);
+            found = 1u;
+            if (!cand) return -1;
+        }
+        // ---- try the next candidate: straight-line, predicated
+        const uint32_t j = (uint32_t)__builtin_ctz(cand);
+        cand &= cand - 1u;
+        const uint32_t cj = evc[j * STRIDE];
+        uint32_t r, pmj = 0u;
+        bool has;                              // findResponse => [] : no child
+        if (is_paired<MODE>()) {
+            r = c_r(cj);
+            has = r != 0u;
+        } else {
+            pmj = same_pid(j);
+            const uint32_t rr = rem & pmj & RESP;
+            has = rr != 0u;
+            r = (uint32_t)__builtin_ctz(rr | 0x80000000u);
+        }
+        const uint32_t cr = evc[r * STRIDE];
+        const uint32_t code = c_code(cj), rc = c_code(cr);
+        const int32_t m = c_ival(cj), rv = c_rval(cr);
+        bool ok, err;
+        uint32_t stw;
+        if constexpr (BANK) {
+            const uint32_t ia = c_a(cj), ib = c_b(cj);
+            const int32_t bal_a = s_bal[ia][lane], bal_b = s_bal[ib][lane];
+            const uint32_t ex_a = (ex >> ia) & 1u, ex_b = (ex >> ib) & 1u;
+            // post (test/Bank.hs:118-131): invariant && expected response
+            const uint32_t tr = code == QSMD_BANK_TRANSFER ? 1u : 0u;
+            const bool chk = code == QSMD_BANK_CHECK_BALANCE;
+            const uint32_t ge = (ex_a & (bal_a >= m ? 1u : 0u));   // lookup >= Just m
+            const uint32_t exp = (uint32_t)(kBankExp >> (3u * (code * 4u + ex_a * 2u + ge))) & 7u;
+            const bool inv_ok = neg == 0u;
+            err = has & inv_ok & chk & (rc == QSMD_BANK_BALANCE) & !ex_a;   // Map.! raises
+            ok = has & inv_ok & (rc == exp) & (!chk | (rv == bal_a));
+            // next' (test/Bank.hs:92-101) on a, then Transfer's deposit on b;
+            // stored unconditionally (the old values when !ok)
+            stw = j | (ex_a << 5) | (ex_b << 6);
+            const int32_t sa = (int32_t)((kBankPos >> code) & 1u) - (int32_t)((kBankNeg >> code) & 1u);
+            const int32_t na = ex_a ? bal_a + sa * m : (sa != 0 ? m : 0);
+            const uint32_t ex1 = ex | ((chk ? 0u : 1u) << ia);
+            const int32_t bo = ia == ib ? na : bal_b;
+            const int32_t nb = ((ex1 >> ib) & 1u) ? bo + m : m;
+            const int32_t fb = tr ? nb : bo;
+            s_bal[ia][lane] = ok ? na : bal_a;
+            s_bal[ib][lane] = ok ? fb : bal_b;
+            const uint32_t ex2 = ex1 | (tr << ib);
+            const int32_t va = ia == ib ? fb : na;
+            uint32_t neg2 = neg & ~((1u << ia) | (1u << ib));
+            neg2 |= ((va < 0) ? ((ex2 >> ia) & 1u) : 0u) << ia;
+            neg2 |= ((fb < 0) ? ((ex2 >> ib) & 1u) : 0u) << ib;
+            ex = ok ? ex2 : ex;
+            neg = ok ? neg2 : neg;
+        } else {
+            // model at this depth: Just (#TT since the last Reset), or model0
+            // advanced by succ <$> once per level
+            const uint32_t m0_just = a.m0_just;
+            const int32_t m0_n = (int32_t)a.m0_val[0];
+            const uint32_t just = RS ? 1u : m0_just;
+            const int32_t tn = RS ? (int32_t)(depth - 1u - (31u - __builtin_clz(RS | 1u)))
+                                  : m0_n + (m0_just ? (int32_t)depth : 0);
+            // postcondition (test/TicketDispenser.hs:99-102)
+            const bool tt = code == QSMD_TICKET_TAKE_TICKET;
+            err = false;
+            ok = has & (tt ? (rc == QSMD_TICKET_NUMBER) & (just != 0u) & (rv == tn + 1) : rc == QSMD_TICKET_OK);
+            stw = j;
+            RS |= ((ok & !tt) ? 1u : 0u) << depth;   // transition: Reset => Just 0
+        }
+        // budget before the node is counted, then Map.! (rare exit)
+        const bool over = has & (nodes >= limit);
+        if (over | err) {
+            nodes += over ? 0u : 1u;
+            return over ? QSMD_STATUS_BUDGET : QSMD_STATUS_MODEL_ERROR;
+        }
+        nodes += has ? 1u : 0u;
+        found |= has ? 1u : 0u;
+        // descend on success
+        stk.put(ok ? depth : 64u, stw);
+        depth += ok ? 1u : 0u;
+        const uint32_t fi = rem & pmj & INV;
+        const uint32_t rem2 = rem & ~((is_paired<MODE>() ? (1u << j) : (fi & (0u - fi))) | (1u << r));
+        rem = ok ? rem2 : rem;
+        cand = ok ? cands(rem2, INV, RESP) : cand;
+        found = ok ? 0u : found;
+        return -1;
+    }
+
+    __device__ __forceinline__ void write_witness(uint8_t* w, uint32_t n_ev) const {
+        for (uint32_t d = 0; d < depth; ++d) w[d] = (uint8_t)(stk.get(d) & 31u);
+        if (depth < n_ev) w[depth] = QSMD_WITNESS_END;
+    }
+};
+
+__device__ __forceinline__ bool time_up(const SearchArgs& a, uint64_t t0, uint32_t& iter) {
+    return a.time_limit && ((++iter & 1023u) == 0u) && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit;
+}
+
+// Wave-aggregated append of h to list (one atomic per wavefront).
+__device__ __forceinline__ void wave_append(bool pred, uint32_t h, uint32_t* list, uint32_t* count, int lane) {
+    const uint64_t dm = __ballot(pred);
+    if (dm) {
+        const int leader = __builtin_ctzll(dm);
+        uint32_t slot = 0;
+        if (lane == leader) slot = atomicAdd(count, (uint32_t)__builtin_popcountll(dm));
+        slot = __shfl(slot, leader, 64);
+        if (pred) list[slot + lane_prefix(dm)] = h;
+    }
+}
+
+struct Counters {
+    uint32_t lin = 0, nonlin = 0, err = 0, enc = 0, budget = 0;
+    uint64_t nodes = 0;
+    __device__ __forceinline__ void add(int status, uint64_t n) {
+        if (status == QSMD_STATUS_SKIPPED) return;     // counted by early_exit_fixup
+        lin += status == QSMD_STATUS_LINEARISABLE;
+        nonlin += status == QSMD_STATUS_NONLINEARISABLE;
+        err += status == QSMD_STATUS_MODEL_ERROR;
+        enc += status == QSMD_STATUS_ENCODE_ERROR;
+        budget += status == QSMD_STATUS_BUDGET;
+        nodes += n;
+    }
+    __device__ __forceinline__ void flush(unsigned long long* partials, int lane) const {
+        const uint64_t t_lin = wave_sum64(lin), t_non = wave_sum64(nonlin), t_err = wave_sum64(err),
+                       t_enc = wave_sum64(enc), t_bud = wave_sum64(budget), t_nodes = wave_sum64(nodes);
+        if (lane == 0) {
+            unsigned long long* p = partials + (uint64_t)blockIdx.x * T_N;
+            p[T_CHECKED] = t_lin + t_non + t_err;
+            p[T_LIN] = t_lin;
+            p[T_NONLIN] = t_non;
+            p[T_ERR] = t_err;
+            p[T_ENC] = t_enc;
+            p[T_BUDGET] = t_bud;
+            p[T_SKIPPED] = 0;
+            p[T_NODES] = t_nodes;
+        }
+    }
+};
+
+}  // namespace
+
+}  // namespace qsmd

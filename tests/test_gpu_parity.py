@@ -246,3 +246,32 @@ def test_device_resident_full_size(ctx):
     idx = np.arange(0, n, 50)
     st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr[idx], ev, threads=8)
     assert np.array_equal(st_o, st[idx]) and np.array_equal(nd_o, nd[idx])
+
+
+@pytest.mark.parametrize("packed", [True, False])
+def test_value_ranges_and_pairing(ctx, packed):
+    """Stage 0 holds invocation values within 14-bit signed and response
+    values within 25-bit signed; anything wider goes to stage 1.  Put values
+    on both sides of both bounds into generated Bank histories (packed
+    uniform batch and a non-uniform one), and mix paired (every pid
+    alternates) with unpaired histories inside one wavefront."""
+    hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 7, 64 * 40)
+    ev = ev.copy()
+    nr = np.random.default_rng(11)
+    inv = np.nonzero((ev["kp"] & 0x80) == 0)[0]
+    rsp = np.nonzero(((ev["kp"] & 0x80) != 0) & (ev["code"] == 7))[0]        # Balance responses
+    iv = np.array([8191, 8192, -8192, -8193, 1 << 20, -(1 << 30)], dtype=np.int32)
+    rv = np.array([(1 << 24) - 1, 1 << 24, -(1 << 24), -(1 << 24) - 1, 1 << 30], dtype=np.int32)
+    ki = nr.choice(inv, 300, replace=False)
+    kr = nr.choice(rsp, 300, replace=False)
+    ev["val"][ki] = iv[nr.integers(0, len(iv), len(ki))]
+    ev["val"][kr] = rv[nr.integers(0, len(rv), len(kr))]
+    # unpaired: give a few histories a second invocation of the same pid
+    # before its response (and a stray response) by swapping two events
+    for h in nr.choice(len(hdr), 200, replace=False):
+        o = int(hdr[h]["ev_off"])
+        i = o + int(nr.integers(4, 30))
+        ev[[i, i + 1]] = ev[[i + 1, i]]
+    if not packed:
+        hdr = hdr[nr.permutation(len(hdr))]
+    _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**6)
