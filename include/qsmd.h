@@ -294,6 +294,12 @@ int qsmd_combine_tasks(const qsmd_frontier* frontier, const qsmd_task* tasks,
  * HW_ID, XCC_ID).  NULL restores the production kernel. */
 int qsmd_diag_stamps(qsmd_ctx* ctx, void* stamps_dev);
 
+/* Diagnostic: the spread stage (dynamic split of the histories over the
+ * stage-0 node budget) of the most recent call: out4[0] = histories it
+ * searched, [1] = tasks, [2] = nodes explored (speculation included),
+ * [3] = sum of their reference node counts.  Synchronises the device. */
+int qsmd_spread_stats(qsmd_ctx* ctx, uint64_t* out4);
+
 /* Device time (ms, HIP events on the launch stream) of the search kernels of
  * the most recent check call, measured once that stream has completed. */
 int qsmd_last_kernel_ms(qsmd_ctx* ctx, float* ms_out);

@@ -42,6 +42,22 @@ struct qsmd_ctx {
     uint64_t split_budget = 4096;      // per-lane node budget before the split stage (0 = none)
     uint64_t stage0_persistent = 0;    // > 0: stage 0 = persistent refill_search (direct) with this grid
     uint64_t refill_min = 8;           // refill kernels: idle lanes before a wavefront refills
+    uint64_t spread_budget = 128;      // spread stage: nodes a task searches before it splits
+    uint64_t spread_grid = 2048;       // spread stage: persistent wavefronts
+    uint64_t spread_pending = 1024;    // spread stage: split only while fewer tasks wait
+    uint64_t heavy_stage = 2;          // histories over the stage-0 budget: 0 = coop, 1 = spread,
+                                       // 2 = auto (coop for at most coop_max of them, else spread)
+    uint64_t coop_max = 4096;
+    uint64_t coop_grid = 2048;         // coop stage: persistent wavefronts
+    uint64_t coop_budget = 16;         // coop stage: nodes a task searches before it may split
+    uint64_t spread_cap = 1ull << 22;  // spread stage: task records per call (64 B each)
+    uint32_t epoch = 0;                // spread stage: ready-flag value of the current call
+    unsigned long long* spread_stamps = nullptr;   // diagnostic: spread task timeline
+    char* spt = nullptr;               // spread task records (own buffer: zeroed once, then
+    size_t spt_bytes = 0;              // told apart by the epoch of their ready flag)
+    const SpreadHist* last_sp_hist = nullptr;   // diagnostics of the last spread launch
+    const uint32_t* last_sp_count = nullptr;
+    const unsigned long long* last_sp_ad = nullptr;
     // QSMD_FLAG_MEMO table (device), allocated on first use
     unsigned long long* memo = nullptr;
     uint64_t memo_entries = 1ull << 22;
@@ -55,7 +71,8 @@ namespace {
 
 constexpr uint32_t kStage1Grid = 1024;   // list-mode stages: grid-stride
 constexpr uint32_t kStage2Grid = 1024;
-constexpr uint32_t kRefillGrid = 2048;   // persistent: 8 wavefronts per CU
+constexpr uint32_t kRedoGrid = 64;      // exact re-search of spread histories the speculation cap cut
+constexpr uint32_t kSpreadFinalGrid = 64;
 constexpr uint64_t kTimingSlots = 1024;
 constexpr uint32_t kFrontierGrid = 256;  // split stage: one lane per giant history, grid-stride
 constexpr uint32_t kTaskGrid[SPLIT_VARIANTS] = {1024, 512};   // persistent task wavefronts
@@ -163,6 +180,7 @@ void qsmd_close(qsmd_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->ws) (void)hipFree(c->ws);
     if (c->sx) (void)hipFree(c->sx);
+    if (c->spt) (void)hipFree(c->spt);
     if (c->memo) (void)hipFree(c->memo);
     if (c->io) (void)hipFree(c->io);
     for (auto e : c->ev)
@@ -174,6 +192,26 @@ void qsmd_close(qsmd_ctx* c) {
 int qsmd_diag_stamps(qsmd_ctx* c, void* stamps_dev) {
     if (!c) return QSMD_ERR_ARG;
     c->stamps = static_cast<unsigned long long*>(stamps_dev);
+    return QSMD_OK;
+}
+
+int qsmd_spread_stats(qsmd_ctx* c, uint64_t* out4) {
+    if (!c || !out4) return QSMD_ERR_ARG;
+    for (int i = 0; i < 4; ++i) out4[i] = 0;
+    if (!c->last_sp_hist) return QSMD_OK;
+    HIP_TRY(c, hipDeviceSynchronize(), "sync");
+    uint32_t n = 0;
+    unsigned long long ad = 0;
+    HIP_TRY(c, hipMemcpy(&n, c->last_sp_count, 4, hipMemcpyDeviceToHost), "D2H");
+    HIP_TRY(c, hipMemcpy(&ad, c->last_sp_ad, 8, hipMemcpyDeviceToHost), "D2H");
+    std::vector<SpreadHist> h(n);
+    if (n) HIP_TRY(c, hipMemcpy(h.data(), c->last_sp_hist, n * sizeof(SpreadHist), hipMemcpyDeviceToHost), "D2H");
+    out4[0] = n;
+    out4[1] = ad >> 32;
+    for (const auto& r : h) {
+        out4[2] += r.explored;
+        out4[3] += r.sum;
+    }
     return QSMD_OK;
 }
 
@@ -192,6 +230,30 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "refill_min") {
         if (value < 1 || value > 64) return fail(c, QSMD_ERR_ARG, "refill_min in 1..64");
         c->refill_min = value;
+    } else if (n == "spread_budget") {
+        if (value < 1) return fail(c, QSMD_ERR_ARG, "spread_budget >= 1");
+        c->spread_budget = value;
+    } else if (n == "spread_pending") {
+        c->spread_pending = std::min<uint64_t>(value, 0xFFFFFFFFull);
+    } else if (n == "spread_stamps_ptr") {   // diagnostic: device buffer of 4 x u64 per task slot
+        c->spread_stamps = reinterpret_cast<unsigned long long*>(value);
+    } else if (n == "heavy_stage") {
+        if (value > 2) return fail(c, QSMD_ERR_ARG, "heavy_stage: 0 = coop, 1 = spread, 2 = auto");
+        c->heavy_stage = value;
+    } else if (n == "coop_max") {
+        c->coop_max = std::min<uint64_t>(value, 0xFFFFFFFFull);
+    } else if (n == "coop_grid") {
+        if (value < 1 || value > 65536) return fail(c, QSMD_ERR_ARG, "coop_grid in 1..65536");
+        c->coop_grid = value;
+    } else if (n == "coop_budget") {
+        if (value < 1) return fail(c, QSMD_ERR_ARG, "coop_budget >= 1");
+        c->coop_budget = value;
+    } else if (n == "spread_grid") {
+        if (value < 1 || value > 65536) return fail(c, QSMD_ERR_ARG, "spread_grid in 1..65536");
+        c->spread_grid = value;
+    } else if (n == "spread_cap") {
+        if (value < 1024 || value > 0xFFFFFFF0ull) return fail(c, QSMD_ERR_ARG, "spread_cap in 1024..2^32-16");
+        c->spread_cap = value;
     } else if (n == "split_budget") {
         c->split_budget = value;
     } else if (n == "stage0_budget") {
@@ -265,7 +327,13 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const bool persistent = c->stage0_persistent != 0;
     const uint64_t g0 = persistent ? c->stage0_persistent
                                    : std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), c->stage0_max_grid);
-    const uint64_t g0b = c->stage0_budget && !persistent ? kRefillGrid : 0;   // no refill stage without a budget
+    // stage-0 node budget: the histories over it go to the spread stage (and
+    // the ones its speculation cap cut to an exact re-search, kRedoGrid)
+    const bool spread = c->stage0_budget && !persistent && (!max_nodes || c->stage0_budget < max_nodes);
+    const bool coop = spread && c->heavy_stage != 1;
+    const bool use_spread = spread && c->heavy_stage != 0;
+    const uint64_t g_heavy = (coop ? c->coop_grid : 0) + (use_spread ? kSpreadFinalGrid : 0);
+    const uint64_t g0b = spread ? g_heavy + kRedoGrid : 0;
     const uint64_t gfx = early ? std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), 4096) : 0;
     const bool split = c->split_budget && (!max_nodes || c->split_budget < max_nodes);
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
@@ -287,10 +355,18 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const size_t off_ts = off_tk + align_up(n_tk * sizeof(qsmd_task));
     const size_t off_tn = off_ts + align_up(n_tk);
     const size_t off_tw = off_tn + align_up(n_tk * 8);
-    const size_t off_part = off_tw + (want_w ? align_up(n_tk * kTaskWitness) : 0);
+    const size_t off_sh = off_tw + (want_w ? align_up(n_tk * kTaskWitness) : 0);
+    const uint64_t sp_cap = use_spread ? c->spread_cap : 0;
+    const size_t off_sr = off_sh + (spread ? align_up(n_hist * sizeof(SpreadHist)) : 0);
+    const size_t off_part = off_sr + (spread ? align_up(n_hist * 4 + 4) : 0);
     const size_t need = off_part + align_up(n_part * T_N * 8);
     rc = grow(c, &c->ws, &c->ws_bytes, need);
     if (rc) return rc;
+    if (sp_cap && c->spt_bytes < sp_cap * sizeof(SpreadTask)) {
+        rc = grow(c, &c->spt, &c->spt_bytes, sp_cap * sizeof(SpreadTask));
+        if (rc) return rc;
+        HIP_TRY(c, hipMemsetAsync(c->spt, 0, c->spt_bytes, s), "memset spread tasks");
+    }
     uint32_t* cnt = reinterpret_cast<uint32_t*>(c->ws + off_cnt);
     qsmd_totals* tot = totals ? totals : reinterpret_cast<qsmd_totals*>(c->ws + off_tot);
     uint32_t* l0 = reinterpret_cast<uint32_t*>(c->ws + off_l0);
@@ -299,7 +375,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     unsigned long long* part = reinterpret_cast<unsigned long long*>(c->ws + off_part);
     if (early && !nodes) nodes = reinterpret_cast<uint64_t*>(c->ws + off_nd);
 
-    HIP_TRY(c, hipMemsetAsync(cnt, 0, 64, s), "memset counters");
+    HIP_TRY(c, hipMemsetAsync(cnt, 0, 128, s), "memset counters");
     HIP_TRY(c, hipMemsetAsync(cnt + 6, 0xFF, 4, s), "memset first_fail");
     HIP_TRY(c, hipMemsetAsync(tot, 0, sizeof(qsmd_totals), s), "memset totals");
     a.first_fail = early ? cnt + 6 : nullptr;
@@ -334,7 +410,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.defer_count = cnt + 0;
     a0.partials = part;
     a0.stamps = c->stamps;
-    if (c->stage0_budget) {             // stage 0 -> refill -> (split)
+    if (spread) {                       // stage 0 -> spread (-> exact redo)
         a0.heavy_list = lh;
         a0.heavy_count = cnt + 4;
         a0.stage0_budget = c->stage0_budget;
@@ -355,13 +431,60 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         HIP_TRY(c, launch_compact(a0, (uint32_t)g0, s), "stage 0 launch");
     }
     HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
-    // stage 0b: histories over the stage-0 node budget, persistent refill
-    SearchArgs ab = a;
-    ab.list = lh;
-    ab.list_count = cnt + 4;
-    ab.queue_head = cnt + 5;
-    ab.partials = part + g0 * T_N;
-    if (g0b) HIP_TRY(c, launch_refill(ab, (uint32_t)g0b, s), "stage 0b launch");
+    // stage 0b: histories over the stage-0 node budget: one wavefront per
+    // history (coop), or the global dynamic split (spread)
+    if (coop) {
+        CoopArgs cp{};
+        cp.s = a;
+        cp.s.giant_list = nullptr;
+        cp.s.partials = part + g0 * T_N;
+        cp.heavy_list = lh;
+        cp.heavy_count = cnt + 4;
+        cp.next = cnt + 19;
+        cp.budget = c->coop_budget;
+        cp.explore_cap = max_nodes ? 16 * max_nodes + 64 * c->coop_budget : 0;
+        cp.redo_list = reinterpret_cast<uint32_t*>(c->ws + off_sr);
+        cp.redo_count = cnt + 13;
+        cp.stats = c->spread_stamps;
+        cp.max_count = c->heavy_stage == 2 ? (uint32_t)c->coop_max : 0xFFFFFFFFu;
+        HIP_TRY(c, launch_coop(cp, (uint32_t)c->coop_grid, s), "coop launch");
+        c->last_sp_hist = nullptr;
+    }
+    if (use_spread) {
+        SpreadArgs sp{};
+        sp.s = a;
+        sp.s.giant_list = nullptr;      // the spread stage holds every compact history
+        sp.s.partials = part + (g0 + (coop ? c->coop_grid : 0)) * T_N;
+        sp.heavy_list = lh;
+        sp.min_count = c->heavy_stage == 2 ? (uint32_t)c->coop_max + 1u : 0u;
+        sp.heavy_count = cnt + 4;
+        sp.tasks = reinterpret_cast<SpreadTask*>(c->spt);
+        sp.cap = (uint32_t)sp_cap;
+        if (++c->epoch == 0) ++c->epoch;
+        sp.epoch = c->epoch;
+        sp.hist = reinterpret_cast<SpreadHist*>(c->ws + off_sh);
+        sp.ad = reinterpret_cast<unsigned long long*>(cnt + 16);
+        sp.head = cnt + 18;
+        sp.task_budget = c->spread_budget;
+        sp.min_pending = (uint32_t)c->spread_pending;
+        sp.stamps = c->spread_stamps;
+        sp.explore_cap = max_nodes ? 16 * max_nodes + 4 * c->spread_budget : 0;
+        sp.redo_list = reinterpret_cast<uint32_t*>(c->ws + off_sr);
+        sp.redo_count = cnt + 13;
+        HIP_TRY(c, launch_spread(sp, (uint32_t)c->spread_grid, s), "spread launch");
+        c->last_sp_hist = sp.hist;
+        c->last_sp_count = sp.heavy_count;
+        c->last_sp_ad = sp.ad;
+    }
+    if (spread) {
+        SearchArgs ar = a;              // exact per-lane search, no split
+        ar.giant_list = nullptr;
+        ar.list = reinterpret_cast<uint32_t*>(c->ws + off_sr);
+        ar.list_count = cnt + 13;
+        ar.queue_head = cnt + 14;
+        ar.partials = part + (g0 + g_heavy) * T_N;
+        HIP_TRY(c, launch_refill(ar, kRedoGrid, s), "redo launch");
+    }
     // stage 1: histories with 33..64 events
     SearchArgs a1 = a;
     a1.list = l0;

@@ -154,6 +154,76 @@ __host__ __device__ inline int combine_tasks(uint32_t term_status, uint64_t term
     return (int)term_status;
 }
 
+// ------------------------------------------------------------ spread stage
+// Dynamic split of the compact-domain histories that exceed the stage-0
+// node budget (csrc/spread.hip).  A task is a region of one history's
+// reference DFS tree: the subtrees of the remaining candidates `cand` of the
+// node reached by the prefix path[0..depth).  Tasks are keyed by their place
+// in the reference's DFS order (spread.hip, key digits), so the verdict and
+// node count of the single DFS are a fold over the task results in key order.
+struct SpreadTask {             // 64 B, 8 x u64 (published with agent-scope stores)
+    uint32_t g;                 // heavy-history index (history = heavy_list[g])
+    uint32_t cand;              // remaining candidates at the base node (~0u: root)
+    uint8_t depth;              // prefix length = base depth
+    uint8_t found;              // the base node already had a child before `cand`
+    uint8_t status;             // result: QSMD_STATUS_*, or SPREAD_SPLIT / SPREAD_CAP
+    uint8_t wdepth;             // LINEARISABLE: witness path length (path[] = the full path)
+    uint32_t pad;
+    uint64_t key_hi, key_lo;    // DFS-order key
+    uint64_t nodes;             // result: nodes this task counted
+    uint8_t path[16];           // prefix (and, on LINEARISABLE, the full witness path)
+    uint64_t ready;             // = the call's epoch once the record is published
+};
+static_assert(sizeof(SpreadTask) == 64, "SpreadTask is 64 B");
+enum : uint8_t { SPREAD_SPLIT = 6, SPREAD_CAP = 7 };
+
+struct SpreadHist {             // per heavy history
+    uint64_t min_hi, min_lo;    // smallest key of a deciding task
+    uint64_t sum;               // nodes of the tasks up to and including the decider
+    uint64_t explored;          // nodes explored by every task (speculation cap)
+    uint32_t flags;             // 1: incomplete (cap) 2: early-exit skip 4: time limit
+    uint32_t win_status;
+    uint64_t pad;
+};
+
+struct SpreadArgs {
+    SearchArgs s;                 // histories, model0, flags, per-history outputs
+    const uint32_t* heavy_list;
+    const uint32_t* heavy_count;
+    SpreadTask* tasks;
+    uint32_t cap;                 // task capacity
+    uint32_t epoch;               // ready-flag value of this call
+    SpreadHist* hist;
+    unsigned long long* ad;       // (allocated << 32) | done
+    uint32_t* head;               // next task slot to take
+    uint64_t task_budget;         // nodes a task searches before it splits
+    uint64_t explore_cap;         // per-history speculation cap (0 = none)
+    uint32_t min_pending;         // split only while fewer tasks than this wait
+    uint32_t min_count;           // run only when at least this many histories came (auto mode)
+    unsigned long long* stamps;   // diagnostic task timeline (null in production)
+    uint32_t* redo_list;          // histories to search again exactly (cap hit)
+    uint32_t* redo_count;
+};
+
+hipError_t launch_spread(const SpreadArgs& p, uint32_t grid, hipStream_t s);
+
+// ------------------------------------------------------------ coop stage
+// One wavefront per heavy compact history (csrc/coop.hip).
+struct CoopArgs {
+    SearchArgs s;                 // histories, model0, flags, outputs; partials [grid]
+    const uint32_t* heavy_list;
+    const uint32_t* heavy_count;
+    uint32_t* next;               // next heavy history to take (zeroed per call)
+    uint64_t budget;              // nodes a task searches before it may split
+    uint64_t explore_cap;         // per-history speculation cap (0 = none)
+    uint32_t* redo_list;          // histories to search again exactly (cap hit)
+    uint32_t* redo_count;
+    unsigned long long* stats;    // diagnostic: 8 x u64 per workgroup (null in production)
+    uint32_t max_count;           // run only when at most this many histories came (auto mode)
+};
+
+hipError_t launch_coop(const CoopArgs& p, uint32_t grid, hipStream_t s);
+
 // Early exit: relaxed agent-scope read (a stale value only delays skipping).
 __device__ __forceinline__ bool beyond_first_fail(const SearchArgs& a, uint32_t h) {
     return a.first_fail && h > __hip_atomic_load(a.first_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -258,6 +258,42 @@ __device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane,
     s.paired = unpaired == 0u;
 }
 
+// finish_lane for a history shared by the wavefront (csrc/coop.hip): every
+// lane derives the same masks from s_hist[e]; only `writer` ORs the pairs in.
+__device__ __forceinline__ void finish_shared(uint32_t* s_hist, bool writer, uint32_t n_ev, uint32_t n_pid,
+                                              Staged& s) {
+    uint32_t W[C_MAXEV];
+#pragma unroll
+    for (uint32_t e = 0; e < (uint32_t)C_MAXEV; ++e) W[e] = s_hist[e];
+    uint32_t open = 0u, ps_lo = 0u, ps_hi = 0u, unpaired = 0u, bad = 0u, wide = 0u;
+#pragma unroll
+    for (uint32_t e = 0; e < (uint32_t)C_MAXEV; ++e) {
+        if (e >= n_ev) break;
+        const uint32_t w = W[e];
+        const uint32_t bit = 1u << e;
+        const uint32_t p = w & 7u, resp = (w >> 3) & 1u, mk = w & 0x78u;
+        bad |= ((mk == MARK_BAD) | (p >= n_pid)) ? 1u : 0u;
+        wide |= mk == MARK_WIDE ? 1u : 0u;
+        s.RESP |= resp ? bit : 0u;
+        s.INV |= resp ? 0u : bit;
+        s.P0 |= (w & 1u) ? bit : 0u;
+        s.P1 |= (w & 2u) ? bit : 0u;
+        s.P2 |= (w & 4u) ? bit : 0u;
+        const uint32_t ob = (open >> p) & 1u, sh = (p & 3u) * 8u;
+        const bool hi = p >= 4u;
+        const uint32_t j = ((hi ? ps_hi : ps_lo) >> sh) & 31u;
+        unpaired |= resp ? (ob ^ 1u) : ob;
+        open ^= (resp ? ob : (ob ^ 1u)) << p;
+        const uint32_t ins = (ps_lo & ~(0xFFu << sh)) | (e << sh), insh = (ps_hi & ~(0xFFu << sh)) | (e << sh);
+        ps_lo = (!resp && !hi) ? ins : ps_lo;
+        ps_hi = (!resp && hi) ? insh : ps_hi;
+        if (writer && resp && ob) s_hist[j] |= e << 13;
+    }
+    s.ok = bad == 0u;
+    s.fits = wide == 0u;
+    s.paired = unpaired == 0u;
+}
+
 // --------------------------------------------------------------- the DFS
 
 // Per-lane search state (registers) over the history in LDS column `lane`.
@@ -277,6 +313,7 @@ struct LaneDFS {
     uint32_t rem, cand, depth, ex, neg, RS, found;
     uint32_t base;          // depth of the search root (0; the task depth in split_search)
     bool paired;
+    uint32_t last_j;        // candidate of the most recent try (the one a BUDGET return did not count)
     uint64_t nodes;
     Stack16 stk;
 
@@ -309,6 +346,45 @@ struct LaneDFS {
 
     // evc[e * STRIDE] = compressed event e (the lane's LDS column: STRIDE = 64;
     // a history shared by the wavefront: STRIDE = 1)
+    // Undo the last level: restore the parent node's state exactly
+    // (remaining events, model); returns the candidate the level went through.
+    template <int STRIDE, int MODE>
+    __device__ __forceinline__ uint32_t undo(const uint32_t* evc, int32_t (*s_bal)[C_LANES], int lane) {
+        --depth;
+        const uint32_t st = stk.get(depth);
+        const uint32_t j = st & 31u;
+        const uint32_t cj = (BANK || MODE != M_GENERAL) ? evc[j * STRIDE] : 0u;
+        if (is_paired<MODE>()) {
+            rem |= (1u << j) | (1u << c_r(cj));
+        } else {
+            const uint32_t gone = ~rem & same_pid(j);
+            rem |= (1u << (31 - __builtin_clz(gone & INV))) | (1u << (31 - __builtin_clz(gone & RESP)));
+        }
+        if constexpr (BANK) {
+            const uint32_t code = c_code(cj), ia = c_a(cj), ib = c_b(cj);
+            const int32_t m = c_ival(cj);
+            const uint32_t pa = (st >> 5) & 1u, pb = (st >> 6) & 1u;
+            const uint32_t tr = code == QSMD_BANK_TRANSFER ? 1u : 0u;
+            const int32_t ba = s_bal[ia][lane], bb = s_bal[ib][lane];
+            // undo Transfer's deposit on b, then the step on a
+            const int32_t rb = (pb | (ia == ib)) ? bb - m : 0;
+            const int32_t cur_a = (tr & (ia == ib)) ? rb : ba;
+            const int32_t sa = (int32_t)((kBankPos >> code) & 1u) - (int32_t)((kBankNeg >> code) & 1u);
+            const int32_t ra = pa ? cur_a - sa * m : 0;
+            const int32_t fb = tr ? rb : bb;
+            s_bal[ib][lane] = fb;                  // a no-op unless Transfer
+            s_bal[ia][lane] = ra;                  // written last (ia == ib)
+            ex = (ex & ~((1u << ia) | (tr << ib))) | (pa << ia) | ((tr & pb) << ib);
+            const int32_t vb = ia == ib ? ra : fb;
+            neg &= ~((1u << ia) | (1u << ib));
+            neg |= ((ra < 0) ? ((ex >> ia) & 1u) : 0u) << ia;
+            neg |= ((vb < 0) ? ((ex >> ib) & 1u) : 0u) << ib;
+        } else {
+            RS &= ~(1u << depth);
+        }
+        return j;
+    }
+
     template <int MODE>
     __device__ __forceinline__ bool is_paired() const {
         return MODE == M_PAIRED || (MODE == M_LANE && paired);
@@ -323,38 +399,7 @@ struct LaneDFS {
             if (!found || depth == base)
                 return (!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE;
             // ---- backtrack: restore the parent level exactly
-            --depth;
-            const uint32_t st = stk.get(depth);
-            const uint32_t j = st & 31u;
-            const uint32_t cj = (BANK || MODE != M_GENERAL) ? evc[j * STRIDE] : 0u;
-            if (is_paired<MODE>()) {
-                rem |= (1u << j) | (1u << c_r(cj));
-            } else {
-                const uint32_t gone = ~rem & same_pid(j);
-                rem |= (1u << (31 - __builtin_clz(gone & INV))) | (1u << (31 - __builtin_clz(gone & RESP)));
-            }
-            if constexpr (BANK) {
-                const uint32_t code = c_code(cj), ia = c_a(cj), ib = c_b(cj);
-                const int32_t m = c_ival(cj);
-                const uint32_t pa = (st >> 5) & 1u, pb = (st >> 6) & 1u;
-                const uint32_t tr = code == QSMD_BANK_TRANSFER ? 1u : 0u;
-                const int32_t ba = s_bal[ia][lane], bb = s_bal[ib][lane];
-                // undo Transfer's deposit on b, then the step on a
-                const int32_t rb = (pb | (ia == ib)) ? bb - m : 0;
-                const int32_t cur_a = (tr & (ia == ib)) ? rb : ba;
-                const int32_t sa = (int32_t)((kBankPos >> code) & 1u) - (int32_t)((kBankNeg >> code) & 1u);
-                const int32_t ra = pa ? cur_a - sa * m : 0;
-                const int32_t fb = tr ? rb : bb;
-                s_bal[ib][lane] = fb;                  // a no-op unless Transfer
-                s_bal[ia][lane] = ra;                  // written last (ia == ib)
-                ex = (ex & ~((1u << ia) | (tr << ib))) | (pa << ia) | ((tr & pb) << ib);
-                const int32_t vb = ia == ib ? ra : fb;
-                neg &= ~((1u << ia) | (1u << ib));
-                neg |= ((ra < 0) ? ((ex >> ia) & 1u) : 0u) << ia;
-                neg |= ((vb < 0) ? ((ex >> ib) & 1u) : 0u) << ib;
-            } else {
-                RS &= ~(1u << depth);
-            }
+            const uint32_t j = undo<STRIDE, MODE>(evc, s_bal, lane);
             cand = cands(rem, INV, RESP) & ~below32(j + 1u);
             found = 1u;
             if (!cand) return -1;
@@ -362,6 +407,7 @@ struct LaneDFS {
         // ---- try the next candidate: straight-line, predicated
         const uint32_t j = (uint32_t)__builtin_ctz(cand);
         cand &= cand - 1u;
+        last_j = j;
         const uint32_t cj = evc[j * STRIDE];
         uint32_t r, pmj = 0u;
         bool has;                              // findResponse => [] : no child
@@ -377,6 +423,9 @@ struct LaneDFS {
         const uint32_t cr = evc[r * STRIDE];
         const uint32_t code = c_code(cj), rc = c_code(cr);
         const int32_t m = c_ival(cj), rv = c_rval(cr);
+        // budget before the node is counted (a BUDGET return leaves the state
+        // untouched, so the search can go on with a larger limit)
+        const bool over = has & (nodes >= limit);
         bool ok, err;
         uint32_t stw;
         if constexpr (BANK) {
@@ -390,7 +439,7 @@ struct LaneDFS {
             const uint32_t exp = (uint32_t)(kBankExp >> (3u * (code * 4u + ex_a * 2u + ge))) & 7u;
             const bool inv_ok = neg == 0u;
             err = has & inv_ok & chk & (rc == QSMD_BANK_BALANCE) & !ex_a;   // Map.! raises
-            ok = has & inv_ok & (rc == exp) & (!chk | (rv == bal_a));
+            ok = has & !over & inv_ok & (rc == exp) & (!chk | (rv == bal_a));
             // next' (test/Bank.hs:92-101) on a, then Transfer's deposit on b;
             // stored unconditionally (the old values when !ok)
             stw = j | (ex_a << 5) | (ex_b << 6);
@@ -420,12 +469,11 @@ struct LaneDFS {
             // postcondition (test/TicketDispenser.hs:99-102)
             const bool tt = code == QSMD_TICKET_TAKE_TICKET;
             err = false;
-            ok = has & (tt ? (rc == QSMD_TICKET_NUMBER) & (just != 0u) & (rv == tn + 1) : rc == QSMD_TICKET_OK);
+            ok = has & !over & (tt ? (rc == QSMD_TICKET_NUMBER) & (just != 0u) & (rv == tn + 1) : rc == QSMD_TICKET_OK);
             stw = j;
             RS |= ((ok & !tt) ? 1u : 0u) << depth;   // transition: Reset => Just 0
         }
-        // budget before the node is counted, then Map.! (rare exit)
-        const bool over = has & (nodes >= limit);
+        // budget, then Map.! (rare exit)
         if (over | err) {
             nodes += over ? 0u : 1u;
             return over ? QSMD_STATUS_BUDGET : QSMD_STATUS_MODEL_ERROR;

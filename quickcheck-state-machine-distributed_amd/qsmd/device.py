@@ -63,6 +63,7 @@ EXPORTS = {
     "qsmd_set_stage0_grid": (_I, [_P, _U64]),
     "qsmd_set_stage0_budget": (_I, [_P, _U64]),
     "qsmd_diag_stamps": (_I, [_P, _P]),
+    "qsmd_spread_stats": (_I, [_P, _P]),
     "qsmd_check_batch": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P]),
     "qsmd_check_batch_device": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P, _P]),
     "qsmd_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
@@ -255,6 +256,13 @@ class Context:
 
     def set_stage0_budget(self, nodes):
         self._check(self._lib.qsmd_set_stage0_budget(self._h, int(nodes)), "qsmd_set_stage0_budget")
+
+    def spread_stats(self):
+        """Spread stage of the last call: (histories, tasks, explored nodes,
+        sum of their reference node counts)."""
+        out = (ctypes.c_uint64 * 4)()
+        self._check(self._lib.qsmd_spread_stats(self._h, out), "qsmd_spread_stats")
+        return tuple(int(x) for x in out)
 
     def diag_stamps(self, ptr):
         self._check(self._lib.qsmd_diag_stamps(self._h, ptr), "qsmd_diag_stamps")

@@ -275,3 +275,62 @@ def test_value_ranges_and_pairing(ctx, packed):
     if not packed:
         hdr = hdr[nr.permutation(len(hdr))]
     _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**6)
+
+
+HEAVY_DEFAULTS = {"stage0_budget": 0, "heavy_stage": 2, "coop_budget": 16, "spread_budget": 128,
+                  "spread_cap": 1 << 22, "coop_max": 4096}
+
+
+def _heavy(ctx, **kw):
+    for k, v in {**HEAVY_DEFAULTS, **kw}.items():
+        ctx.set_param(k, v)
+
+
+@pytest.mark.parametrize("name,n", [("bank_4x16_bugs", 20000), ("bank_4x16", 20000), ("ticket_2x10", 20000)])
+@pytest.mark.parametrize("stage,task_budget,cap", [("coop", 1, 0), ("coop", 4, 0), ("coop", 64, 0),
+                                                   ("spread", 4, 1 << 22), ("spread", 128, 1 << 22),
+                                                   ("spread", 8, 1024), ("auto-coop", 16, 0),
+                                                   ("auto-spread", 64, 1 << 22)])
+def test_heavy_stage(ctx, name, n, stage, task_budget, cap):
+    """The stages for the histories over the stage-0 node budget: coop (one
+    wavefront per history, csrc/coop.hip) and spread (global dynamic split,
+    csrc/spread.hip).  Tiny task budgets force deep split trees; a tiny
+    spread capacity forces its 'no room: search on' path.  Verdicts, node
+    counts and witnesses must be exactly the single DFS's."""
+    hdr, ev, _ = gen.generate_config(name, 3, n)
+    if stage == "coop":
+        _heavy(ctx, stage0_budget=8, heavy_stage=0, coop_budget=task_budget)
+    elif stage == "spread":
+        _heavy(ctx, stage0_budget=8, heavy_stage=1, spread_budget=task_budget, spread_cap=cap)
+    else:                                        # auto: the count decides (1 history -> spread)
+        _heavy(ctx, stage0_budget=8, heavy_stage=2, coop_budget=task_budget, spread_budget=task_budget,
+               coop_max=1 << 20 if stage == "auto-coop" else 0)
+    try:
+        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev)
+    finally:
+        _heavy(ctx)
+
+
+@pytest.mark.parametrize("model", ["ticket", "bank"])
+@pytest.mark.parametrize("stage", ["coop", "spread"])
+def test_heavy_any_shape(ctx, model, stage):
+    """Shared pids, pending invocations, stray responses, Map.! errors and
+    node budgets through the heavy stages (general, unpaired search)."""
+    rng = random.Random(77 if model == "ticket" else 78)
+    hs = []
+    for _ in range(4000):
+        if rng.random() < 0.5:
+            hs.append(histgen.random_history(rng, model, rng.randint(8, 32), rng.randint(1, 3)))
+        else:
+            hs.append(histgen.wellformed_history(rng, model, rng.randint(6, 16), rng.randint(2, 6)))
+    m = models.BY_NAME[model]
+    b = codec.encode(m, hs)
+    if stage == "coop":
+        _heavy(ctx, stage0_budget=4, heavy_stage=0, coop_budget=2)
+    else:
+        _heavy(ctx, stage0_budget=4, heavy_stage=1, spread_budget=6)
+    try:
+        for max_nodes in (0, 50, 3000):
+            _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=max_nodes)
+    finally:
+        _heavy(ctx)
