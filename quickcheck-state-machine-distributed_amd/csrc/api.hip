@@ -48,6 +48,14 @@ struct qsmd_ctx {
     uint64_t heavy_stage = 2;          // histories over the stage-0 budget: 0 = coop, 1 = spread,
                                        // 2 = auto (coop for at most coop_max of them, else spread)
     uint64_t coop_max = 4096;
+    uint64_t stage0_kernel = 0;        // 0 = compact_search, 1 = group_search (in-wave sharing)
+    uint64_t stage0_dynamic = 0;       // compact_search: groups from a counter (persistent grid)
+    uint64_t group_grid = 4096;        // group_search: persistent wavefronts (cap)
+    uint64_t group_budget = 16;        // group_search: nodes a shared task searches before it may split
+    uint64_t share_idle = 16;          // group_search: idle lanes that start sharing
+    uint64_t share_nodes = 32;         // group_search: nodes a search must have counted to be shared
+    unsigned long long* group_stats = nullptr;
+    unsigned long long* group_debug = nullptr;
     uint64_t coop_grid = 2048;         // coop stage: persistent wavefronts
     uint64_t coop_budget = 16;         // coop stage: nodes a task searches before it may split
     uint64_t spread_cap = 1ull << 22;  // spread stage: task records per call (64 B each)
@@ -237,6 +245,26 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->spread_pending = std::min<uint64_t>(value, 0xFFFFFFFFull);
     } else if (n == "spread_stamps_ptr") {   // diagnostic: device buffer of 4 x u64 per task slot
         c->spread_stamps = reinterpret_cast<unsigned long long*>(value);
+    } else if (n == "stage0_kernel") {
+        if (value > 1) return fail(c, QSMD_ERR_ARG, "stage0_kernel: 0 = compact, 1 = group");
+        c->stage0_kernel = value;
+    } else if (n == "stage0_dynamic") {
+        c->stage0_dynamic = value ? 1 : 0;
+    } else if (n == "group_grid") {
+        if (value < 1 || value > 65536) return fail(c, QSMD_ERR_ARG, "group_grid in 1..65536");
+        c->group_grid = value;
+    } else if (n == "group_budget") {
+        if (value < 1) return fail(c, QSMD_ERR_ARG, "group_budget >= 1");
+        c->group_budget = value;
+    } else if (n == "share_idle") {
+        if (value < 1 || value > 64) return fail(c, QSMD_ERR_ARG, "share_idle in 1..64");
+        c->share_idle = value;
+    } else if (n == "share_nodes") {
+        c->share_nodes = std::min<uint64_t>(value, 0xFFFFFFFFull);
+    } else if (n == "group_debug_ptr") {    // diagnostic: device buffer of 256 x u64 per block
+        c->group_debug = reinterpret_cast<unsigned long long*>(value);
+    } else if (n == "group_stats_ptr") {    // diagnostic: device buffer of 8 x u64 per group_search block
+        c->group_stats = reinterpret_cast<unsigned long long*>(value);
     } else if (n == "heavy_stage") {
         if (value > 2) return fail(c, QSMD_ERR_ARG, "heavy_stage: 0 = coop, 1 = spread, 2 = auto");
         c->heavy_stage = value;
@@ -325,15 +353,20 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
 
     // ---- workspace: defer lists, counters, partials, internal totals
     const bool persistent = c->stage0_persistent != 0;
+    const bool grp = c->stage0_kernel == 1 && !persistent;   // group_search (in-wave sharing)
+    const uint64_t n_groups = std::max<uint64_t>((n_hist + 63) / 64, 1);
     const uint64_t g0 = persistent ? c->stage0_persistent
-                                   : std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), c->stage0_max_grid);
-    // stage-0 node budget: the histories over it go to the spread stage (and
-    // the ones its speculation cap cut to an exact re-search, kRedoGrid)
-    const bool spread = c->stage0_budget && !persistent && (!max_nodes || c->stage0_budget < max_nodes);
+                        : grp      ? std::min<uint64_t>(n_groups, c->group_grid)
+                                   : std::min<uint64_t>(n_groups, c->stage0_max_grid);
+    // stage-0 node budget (compact_search): the histories over it go to the
+    // heavy stages (and the ones a speculation cap cut to an exact
+    // re-search, kRedoGrid); group_search shares them in-wave instead
+    const bool spread = !grp && c->stage0_budget && !persistent && (!max_nodes || c->stage0_budget < max_nodes);
+    const bool grp_redo = grp && max_nodes;
     const bool coop = spread && c->heavy_stage != 1;
     const bool use_spread = spread && c->heavy_stage != 0;
     const uint64_t g_heavy = (coop ? c->coop_grid : 0) + (use_spread ? kSpreadFinalGrid : 0);
-    const uint64_t g0b = spread ? g_heavy + kRedoGrid : 0;
+    const uint64_t g0b = spread ? g_heavy + kRedoGrid : (grp_redo ? kRedoGrid : 0);
     const uint64_t gfx = early ? std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), 4096) : 0;
     const bool split = c->split_budget && (!max_nodes || c->split_budget < max_nodes);
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
@@ -358,7 +391,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const size_t off_sh = off_tw + (want_w ? align_up(n_tk * kTaskWitness) : 0);
     const uint64_t sp_cap = use_spread ? c->spread_cap : 0;
     const size_t off_sr = off_sh + (spread ? align_up(n_hist * sizeof(SpreadHist)) : 0);
-    const size_t off_part = off_sr + (spread ? align_up(n_hist * 4 + 4) : 0);
+    const size_t off_gs = off_sr + ((spread || grp_redo) ? align_up(n_hist * 4 + 4) : 0);
+    const size_t off_part = off_gs + (grp ? align_up(g0 * sizeof(GroupScratch)) : 0);
     const size_t need = off_part + align_up(n_part * T_N * 8);
     rc = grow(c, &c->ws, &c->ws_bytes, need);
     if (rc) return rc;
@@ -428,7 +462,26 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         ad.partials = part;
         HIP_TRY(c, launch_refill(ad, (uint32_t)g0, s), "stage 0 (persistent) launch");
     } else {
-        HIP_TRY(c, launch_compact(a0, (uint32_t)g0, s), "stage 0 launch");
+        if (grp) {
+            GroupArgs gp{};
+            gp.s = a0;
+            gp.s.heavy_list = nullptr;
+            gp.s.giant_list = nullptr;
+            gp.scratch = reinterpret_cast<GroupScratch*>(c->ws + off_gs);
+            gp.group_next = cnt + 20;
+            gp.task_budget = c->group_budget;
+            gp.share_idle = (uint32_t)c->share_idle;
+            gp.share_nodes = (uint32_t)c->share_nodes;
+            gp.explore_cap = max_nodes ? 16 * max_nodes + 64 * c->group_budget : 0;
+            gp.redo_list = reinterpret_cast<uint32_t*>(c->ws + off_sr);
+            gp.redo_count = cnt + 13;
+            gp.stats = c->group_stats;
+            gp.debug = c->group_debug;
+            HIP_TRY(c, launch_group(gp, (uint32_t)g0, s), "stage 0 (group) launch");
+        } else {
+            a0.queue_head = c->stage0_dynamic ? cnt + 21 : nullptr;
+            HIP_TRY(c, launch_compact(a0, (uint32_t)g0, s), "stage 0 launch");
+        }
     }
     HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
     // stage 0b: histories over the stage-0 node budget: one wavefront per
@@ -476,7 +529,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         c->last_sp_count = sp.heavy_count;
         c->last_sp_ad = sp.ad;
     }
-    if (spread) {
+    if (spread || grp_redo) {
         SearchArgs ar = a;              // exact per-lane search, no split
         ar.giant_list = nullptr;
         ar.list = reinterpret_cast<uint32_t*>(c->ws + off_sr);

@@ -79,8 +79,11 @@ __global__ __launch_bounds__(C_LANES, 4) void compact_search(SearchArgs a) {
     uint64_t st_acc[4] = {0, 0, 0, 0}, ts_a = 0, ts_b = 0;
     const uint64_t rt0 = STAMP ? __builtin_amdgcn_s_memrealtime() : 0;
 
-    for (uint64_t base = (uint64_t)blockIdx.x * C_LANES; base < total;
-         base += (uint64_t)gridDim.x * C_LANES) {
+    // groups of 64 histories: this block's first, then (a.queue_head set)
+    // dynamically from a counter fetched one group ahead, else grid-stride
+    uint32_t next = 0;
+    if (a.queue_head && lane == 0) next = atomicAdd(a.queue_head, 1u) + gridDim.x;
+    for (uint64_t base = (uint64_t)blockIdx.x * C_LANES; base < total;) {
         if constexpr (STAMP) ts_a = __builtin_amdgcn_s_memtime();
         const uint64_t idx = base + lane;
         const bool active = idx < total;
@@ -109,7 +112,18 @@ __global__ __launch_bounds__(C_LANES, 4) void compact_search(SearchArgs a) {
             st_acc[0] += ts_b - ts_a;
         }
         wave_append(defer, h, a.defer_list, a.defer_count, lane);   // -> stage 1
-        if (!active || defer) continue;
+        // the next group (uniform): counted ahead, or grid-stride
+        uint64_t base_next;
+        if (a.queue_head) {
+            base_next = (uint64_t)(uint32_t)__shfl((int)next, 0, 64) * C_LANES;
+            if (lane == 0 && base_next < total) next = atomicAdd(a.queue_head, 1u) + gridDim.x;
+        } else {
+            base_next = base + (uint64_t)gridDim.x * C_LANES;
+        }
+        if (!active || defer) {
+            base = base_next;
+            continue;
+        }
 
         int status = -1;
         LaneDFS<MODEL> dfs;
@@ -141,7 +155,10 @@ __global__ __launch_bounds__(C_LANES, 4) void compact_search(SearchArgs a) {
         // over the stage-0 budget (not the caller's): restart in the refill stage
         const bool heavy = tiered && status == QSMD_STATUS_BUDGET && dfs.nodes >= limit;
         wave_append(heavy, h, a.heavy_list, a.heavy_count, lane);
-        if (heavy) continue;
+        if (heavy) {
+            base = base_next;
+            continue;
+        }
 
         a.status[h] = (uint8_t)status;
         if (a.nodes) a.nodes[h] = dfs.nodes;
@@ -151,6 +168,7 @@ __global__ __launch_bounds__(C_LANES, 4) void compact_search(SearchArgs a) {
             st_acc[2] += __builtin_amdgcn_s_memtime() - ts_a;
             st_acc[3] += 1;
         }
+        base = base_next;
     }
     if constexpr (STAMP) {
         if (lane == 0) {

@@ -224,6 +224,34 @@ struct CoopArgs {
 
 hipError_t launch_coop(const CoopArgs& p, uint32_t grid, hipStream_t s);
 
+// ------------------------------------------------------------ group stage
+// Stage 0 with in-wavefront sharing (csrc/group.hip).  Per-wavefront scratch
+// (global memory, touched by its own wavefront only): the task pool and the
+// task records of the group's shared history.
+struct GroupScratch {
+    static constexpr uint32_t kPool = 64, kRec = 256;
+    uint32_t cand[kPool], meta[kPool], rem[kPool], model[kPool], stk[4][kPool];
+    uint64_t khi[kPool], klo[kPool];
+    int32_t bal[QSMD_BANK_MAX_ACCOUNTS][kPool];
+    uint64_t rkhi[kRec], rklo[kRec], rnodes[kRec];
+};
+
+struct GroupArgs {
+    SearchArgs s;                 // histories, outputs, defer list (-> stage 1); partials [grid]
+    GroupScratch* scratch;        // [grid]
+    uint32_t* group_next;         // group counter (zeroed per call)
+    uint64_t task_budget;         // nodes a shared task searches before it may split
+    uint32_t share_idle;          // idle lanes needed to start sharing
+    uint32_t share_nodes;         // nodes an own search must have counted to be shared
+    uint64_t explore_cap;         // per-history speculation cap (0 = none)
+    uint32_t* redo_list;          // shared histories to search again exactly (cap hit)
+    uint32_t* redo_count;
+    unsigned long long* stats;    // diagnostic: 8 x u64 per workgroup (null in production)
+    unsigned long long* debug;    // diagnostic: 256 x u64 per workgroup (null in production)
+};
+
+hipError_t launch_group(const GroupArgs& p, uint32_t grid, hipStream_t s);
+
 // Early exit: relaxed agent-scope read (a stale value only delays skipping).
 __device__ __forceinline__ bool beyond_first_fail(const SearchArgs& a, uint32_t h) {
     return a.first_fail && h > __hip_atomic_load(a.first_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -129,15 +129,27 @@ def test_mixed_sizes_one_batch(ctx):
 @pytest.mark.parametrize("name,n", [("ticket_2x10", 20000), ("bank_4x16", 50000),
                                     ("bank_4x16_bugs", 50000), ("bank_6x24", 20000)])
 @pytest.mark.parametrize("budget", [0, 24])
-def test_generated_configs(ctx, name, n, budget):
-    """budget > 0: histories over the stage-0 node budget are searched again by
-    the persistent refill stage (csrc/compact.hip refill_search)."""
+@pytest.mark.parametrize("kernel", [0, 1, 2])
+def test_generated_configs(ctx, name, n, budget, kernel):
+    """kernel 0: compact_search (2: with groups from a counter on a
+    persistent grid); budget > 0: histories over the stage-0 node budget go
+    to the heavy stages.  kernel 1: group_search (in-wave sharing; the budget
+    does not apply)."""
+    if kernel == 1 and budget:
+        pytest.skip("group_search has no stage-0 budget")
+    ctx.set_param("stage0_kernel", 1 if kernel == 1 else 0)
+    ctx.set_param("stage0_dynamic", 1 if kernel == 2 else 0)
+    if kernel == 2:
+        ctx.set_param("stage0_grid", 97)
     ctx.set_stage0_budget(budget)
     try:
         hdr, ev, bug = gen.generate_config(name, 0, n)
         st, nd, _ = _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
     finally:
         ctx.set_stage0_budget(0)
+        ctx.set_param("stage0_kernel", 0)
+        ctx.set_param("stage0_dynamic", 0)
+        ctx.set_param("stage0_grid", 65536)
     if name in ("bank_4x16", "bank_6x24"):
         assert (st == codec.STATUS_LIN).all()
 
@@ -278,7 +290,8 @@ def test_value_ranges_and_pairing(ctx, packed):
 
 
 HEAVY_DEFAULTS = {"stage0_budget": 0, "heavy_stage": 2, "coop_budget": 16, "spread_budget": 128,
-                  "spread_cap": 1 << 22, "coop_max": 4096}
+                  "spread_cap": 1 << 22, "coop_max": 4096, "stage0_kernel": 0, "group_budget": 16,
+                  "share_idle": 16, "share_nodes": 32}
 
 
 def _heavy(ctx, **kw):
@@ -290,7 +303,8 @@ def _heavy(ctx, **kw):
 @pytest.mark.parametrize("stage,task_budget,cap", [("coop", 1, 0), ("coop", 4, 0), ("coop", 64, 0),
                                                    ("spread", 4, 1 << 22), ("spread", 128, 1 << 22),
                                                    ("spread", 8, 1024), ("auto-coop", 16, 0),
-                                                   ("auto-spread", 64, 1 << 22)])
+                                                   ("auto-spread", 64, 1 << 22), ("group", 1, 0),
+                                                   ("group", 4, 0), ("group", 16, 0), ("group", 64, 0)])
 def test_heavy_stage(ctx, name, n, stage, task_budget, cap):
     """The stages for the histories over the stage-0 node budget: coop (one
     wavefront per history, csrc/coop.hip) and spread (global dynamic split,
@@ -299,12 +313,14 @@ def test_heavy_stage(ctx, name, n, stage, task_budget, cap):
     counts and witnesses must be exactly the single DFS's."""
     hdr, ev, _ = gen.generate_config(name, 3, n)
     if stage == "coop":
-        _heavy(ctx, stage0_budget=8, heavy_stage=0, coop_budget=task_budget)
+        _heavy(ctx, stage0_kernel=0, stage0_budget=8, heavy_stage=0, coop_budget=task_budget)
     elif stage == "spread":
-        _heavy(ctx, stage0_budget=8, heavy_stage=1, spread_budget=task_budget, spread_cap=cap)
+        _heavy(ctx, stage0_kernel=0, stage0_budget=8, heavy_stage=1, spread_budget=task_budget, spread_cap=cap)
+    elif stage == "group":
+        _heavy(ctx, stage0_kernel=1, group_budget=task_budget, share_idle=1 + task_budget % 7, share_nodes=2)
     else:                                        # auto: the count decides (1 history -> spread)
-        _heavy(ctx, stage0_budget=8, heavy_stage=2, coop_budget=task_budget, spread_budget=task_budget,
-               coop_max=1 << 20 if stage == "auto-coop" else 0)
+        _heavy(ctx, stage0_kernel=0, stage0_budget=8, heavy_stage=2, coop_budget=task_budget,
+               spread_budget=task_budget, coop_max=1 << 20 if stage == "auto-coop" else 0)
     try:
         _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev)
     finally:
@@ -312,7 +328,7 @@ def test_heavy_stage(ctx, name, n, stage, task_budget, cap):
 
 
 @pytest.mark.parametrize("model", ["ticket", "bank"])
-@pytest.mark.parametrize("stage", ["coop", "spread"])
+@pytest.mark.parametrize("stage", ["coop", "spread", "group"])
 def test_heavy_any_shape(ctx, model, stage):
     """Shared pids, pending invocations, stray responses, Map.! errors and
     node budgets through the heavy stages (general, unpaired search)."""
@@ -326,9 +342,11 @@ def test_heavy_any_shape(ctx, model, stage):
     m = models.BY_NAME[model]
     b = codec.encode(m, hs)
     if stage == "coop":
-        _heavy(ctx, stage0_budget=4, heavy_stage=0, coop_budget=2)
+        _heavy(ctx, stage0_kernel=0, stage0_budget=4, heavy_stage=0, coop_budget=2)
+    elif stage == "spread":
+        _heavy(ctx, stage0_kernel=0, stage0_budget=4, heavy_stage=1, spread_budget=6)
     else:
-        _heavy(ctx, stage0_budget=4, heavy_stage=1, spread_budget=6)
+        _heavy(ctx, stage0_kernel=1, group_budget=3, share_idle=2, share_nodes=3)
     try:
         for max_nodes in (0, 50, 3000):
             _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=max_nodes)
