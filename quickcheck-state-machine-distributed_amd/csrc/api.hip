@@ -38,12 +38,23 @@ struct qsmd_ctx {
     uint64_t time_limit_ms = 120000;   // safety net per search launch
     uint64_t stage0_max_grid = 65536;  // tuning: cap on stage-0 workgroups (grid-stride beyond)
     unsigned long long* stamps = nullptr;   // diagnostic: stage-0 phase timings
-    uint64_t stage0_budget = 0;        // stage-0 node budget before the refill stage (0 = none)
+    uint64_t stage0_budget = 0;        // stage-0 node budget before the heavy stages (0 = none)
+    // adaptive cascade (default): each call probes how many of its histories
+    // needed more than kAutoBudget nodes; while the last probe read back says
+    // they are common (>= 1 in kAutoFrac), calls run stage 0 with that budget
+    // and the heavy stages, else without (no heavy-stage launches).  Only the
+    // speed changes, never a result.  An explicit stage-0 budget turns it off.
+    bool stage0_auto = true;
+    bool auto_heavy = false;
+    bool probe_pending = false;
+    uint64_t probe_n_hist = 0;
+    uint32_t* probe_host = nullptr;    // pinned
+    hipEvent_t probe_ev = nullptr;
     uint64_t split_budget = 4096;      // per-lane node budget before the split stage (0 = none)
     uint64_t stage0_persistent = 0;    // > 0: stage 0 = persistent refill_search (direct) with this grid
     uint64_t refill_min = 8;           // refill kernels: idle lanes before a wavefront refills
-    uint64_t spread_budget = 128;      // spread stage: nodes a task searches before it splits
-    uint64_t spread_grid = 2048;       // spread stage: persistent wavefronts
+    uint64_t spread_budget = 1024;     // spread stage: nodes a task searches before it splits
+    uint64_t spread_grid = 1024;       // spread stage: persistent wavefronts
     uint64_t spread_pending = 1024;    // spread stage: split only while fewer tasks wait
     uint64_t heavy_stage = 2;          // histories over the stage-0 budget: 0 = coop, 1 = spread,
                                        // 2 = auto (coop for at most coop_max of them, else spread)
@@ -81,6 +92,8 @@ constexpr uint32_t kStage1Grid = 1024;   // list-mode stages: grid-stride
 constexpr uint32_t kStage2Grid = 1024;
 constexpr uint32_t kRedoGrid = 64;      // exact re-search of spread histories the speculation cap cut
 constexpr uint32_t kSpreadFinalGrid = 64;
+constexpr uint64_t kAutoBudget = 256;    // adaptive cascade: stage-0 budget when long searches are common
+constexpr uint64_t kAutoFrac = 1000;     // ... i.e. at least 1 history in kAutoFrac needs more
 constexpr uint64_t kTimingSlots = 1024;
 constexpr uint32_t kFrontierGrid = 256;  // split stage: one lane per giant history, grid-stride
 constexpr uint32_t kTaskGrid[SPLIT_VARIANTS] = {1024, 512};   // persistent task wavefronts
@@ -178,6 +191,11 @@ int qsmd_open(qsmd_ctx** out, int device) {
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
+    if (hipEventCreateWithFlags(&c->probe_ev, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&c->probe_host), 8, hipHostMallocDefault) != hipSuccess) {
+        qsmd_close(c);
+        return QSMD_ERR_DEVICE;
+    }
     *out = c;
     return QSMD_OK;
 }
@@ -193,6 +211,8 @@ void qsmd_close(qsmd_ctx* c) {
     if (c->io) (void)hipFree(c->io);
     for (auto e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->probe_ev) (void)hipEventDestroy(c->probe_ev);
+    if (c->probe_host) (void)hipHostFree(c->probe_host);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -226,6 +246,7 @@ int qsmd_spread_stats(qsmd_ctx* c, uint64_t* out4) {
 int qsmd_set_stage0_budget(qsmd_ctx* c, uint64_t nodes) {
     if (!c) return QSMD_ERR_ARG;
     c->stage0_budget = nodes;
+    c->stage0_auto = false;
     return QSMD_OK;
 }
 
@@ -286,6 +307,9 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->split_budget = value;
     } else if (n == "stage0_budget") {
         c->stage0_budget = value;
+        c->stage0_auto = false;
+    } else if (n == "stage0_auto") {
+        c->stage0_auto = value != 0;
     } else if (n == "stage0_grid") {
         if (value == 0 || value > 0x7FFFFFFFull) return fail(c, QSMD_ERR_ARG, "bad grid");
         c->stage0_max_grid = value;
@@ -361,7 +385,14 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // stage-0 node budget (compact_search): the histories over it go to the
     // heavy stages (and the ones a speculation cap cut to an exact
     // re-search, kRedoGrid); group_search shares them in-wave instead
-    const bool spread = !grp && c->stage0_budget && !persistent && (!max_nodes || c->stage0_budget < max_nodes);
+    // adaptive cascade: the decision of the last probe that has landed
+    if (c->stage0_auto && c->probe_pending && hipEventQuery(c->probe_ev) == hipSuccess) {
+        c->auto_heavy = (uint64_t)c->probe_host[0] * kAutoFrac >= std::max<uint64_t>(c->probe_n_hist, 1);
+        c->probe_pending = false;
+    }
+    const uint64_t budget0 = c->stage0_auto ? (c->auto_heavy ? kAutoBudget : 0) : c->stage0_budget;
+    const bool probe = c->stage0_auto && !grp && !persistent && !c->probe_pending;
+    const bool spread = !grp && budget0 && !persistent && (!max_nodes || budget0 < max_nodes);
     const bool grp_redo = grp && max_nodes;
     const bool coop = spread && c->heavy_stage != 1;
     const bool use_spread = spread && c->heavy_stage != 0;
@@ -444,10 +475,14 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.defer_count = cnt + 0;
     a0.partials = part;
     a0.stamps = c->stamps;
+    if (probe && !spread) {             // no budget this call: count the long searches
+        a0.probe = cnt + 22;
+        a0.probe_nodes = kAutoBudget;
+    }
     if (spread) {                       // stage 0 -> spread (-> exact redo)
         a0.heavy_list = lh;
         a0.heavy_count = cnt + 4;
-        a0.stage0_budget = c->stage0_budget;
+        a0.stage0_budget = budget0;
     } else if (split) {                 // stage 0 -> split
         a0.heavy_list = lg;
         a0.heavy_count = cnt + 7;
@@ -590,6 +625,13 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         HIP_TRY(c, launch_reduce(part, n_part, tot, s), "reduce launch");
     }
     HIP_TRY(c, hipEventRecord(evs[2], s), "hipEventRecord");
+    if (probe) {                        // heavy mode: the heavy list is the probe
+        HIP_TRY(c, hipMemcpyAsync(c->probe_host, spread ? cnt + 4 : cnt + 22, 4, hipMemcpyDeviceToHost, s),
+                "probe read-back");
+        HIP_TRY(c, hipEventRecord(c->probe_ev, s), "hipEventRecord");
+        c->probe_pending = true;
+        c->probe_n_hist = n_hist;
+    }
     c->n_calls++;
     c->timed = true;
     return QSMD_OK;

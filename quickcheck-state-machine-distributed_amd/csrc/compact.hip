@@ -164,6 +164,10 @@ __global__ __launch_bounds__(C_LANES, 4) void compact_search(SearchArgs a) {
         if (a.nodes) a.nodes[h] = dfs.nodes;
         if (a.witness && status == QSMD_STATUS_LINEARISABLE) dfs.write_witness(a.witness + H.ev_off, n_ev);
         cnt.add(status, dfs.nodes);
+        if (a.probe) {                            // adaptive cascade (api.hip): long searches
+            const uint64_t pm = __ballot(dfs.nodes > a.probe_nodes);
+            if (pm && lane == __builtin_ctzll(pm)) atomicAdd(a.probe, (uint32_t)__builtin_popcountll(pm));
+        }
         if constexpr (STAMP) {
             st_acc[2] += __builtin_amdgcn_s_memtime() - ts_a;
             st_acc[3] += 1;

@@ -57,6 +57,10 @@ struct SearchArgs {
     uint32_t* giant_list;
     uint32_t* giant_count;
     uint64_t split_budget;
+    // adaptive cascade probe: histories whose search counted more than
+    // probe_nodes nodes (null = no probe)
+    uint32_t* probe;
+    uint64_t probe_nodes;
 };
 
 // The per-lane node limit of a stage, and whether reaching it hands the

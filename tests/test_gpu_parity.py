@@ -352,3 +352,18 @@ def test_heavy_any_shape(ctx, model, stage):
             _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=max_nodes)
     finally:
         _heavy(ctx)
+
+
+def test_adaptive_cascade(ctx):
+    """The default adaptive cascade: a call's probe (histories needing more
+    than 256 nodes) decides whether later calls run stage 0 with a node budget
+    and the heavy stages.  Results are exact in both modes and across the
+    switches (bug-heavy batch, then a clean one, then the bug-heavy again)."""
+    ctx.set_param("stage0_auto", 1)
+    try:
+        b3 = gen.generate_config("bank_4x16_bugs", 11, 30000)
+        b2 = gen.generate_config("bank_4x16", 11, 30000)
+        for hdr, ev, _ in (b3, b3, b3, b2, b2, b3):
+            _compare(ctx, models.MODEL_BANK, hdr, ev)
+    finally:
+        ctx.set_stage0_budget(0)

@@ -16,7 +16,7 @@ import torch  # noqa: E402
 
 from qsmd import device, gen  # noqa: E402
 
-DEFAULTS = {"stage0_budget": 0, "spread_budget": 128, "spread_grid": 2048, "refill_min": 8, "heavy_stage": 2,
+DEFAULTS = {"stage0_auto": 1, "spread_budget": 1024, "spread_grid": 1024, "refill_min": 8, "heavy_stage": 2,
             "coop_budget": 16, "coop_grid": 2048}
 
 
