@@ -287,6 +287,44 @@ int qsmd_combine_tasks(const qsmd_frontier* frontier, const qsmd_task* tasks,
                        uint64_t max_nodes, uint8_t* status_out, uint64_t* nodes_out,
                        int64_t* winner_out);
 
+/* ------------------------------------------------------------ wellformed
+ *
+ * Batched `wellformed pids history` (src/Linearisability.hs:97-135; call
+ * site test/Bank.hs:281-283): every listed pid's subhistory must be
+ * sequential; the result is the first NotSequential error in `pids` order,
+ * as the constructor code, the pid and the history-local indices of the
+ * events it names (ev0 = the first, ev1 = the second; equal when it names
+ * one).  InvocationFollowedByNonMatchingResponse compares the pids of one
+ * subhistory, which are equal, so wellformed never returns it. */
+typedef struct qsmd_wf {
+    uint8_t  code;      /* QSMD_WF_*                                         */
+    uint8_t  pid;       /* dense pid of the failing subhistory               */
+    uint16_t ev0;
+    uint16_t ev1;
+    uint16_t reserved;
+} qsmd_wf;
+
+#define QSMD_WF_OK                                         0u
+#define QSMD_WF_FIRST_EVENT_ISNT_INVOCATION                1u
+#define QSMD_WF_INVOCATION_FOLLOWED_BY_INVOCATION          2u
+#define QSMD_WF_INVOCATION_FOLLOWED_BY_NON_MATCHING_RESPONSE 3u
+#define QSMD_WF_RESPONSE_FOLLOWED_BY_RESPONSE              4u
+#define QSMD_WF_RESPONSE_FOLLOWED_BY_INVOCATION            5u
+#define QSMD_WF_LONE_RESPONSE                              6u
+#define QSMD_WF_ENCODE_ERROR                               0xFEu
+
+/* pids: the `pids` list as dense pid indices (< 128, each at most once),
+ * applied to every history; NULL = all pids in order 0, 1, 2, ...
+ * Host buffers, synchronous. */
+int qsmd_wellformed_batch(qsmd_ctx* ctx, const qsmd_hdr* hdr, uint64_t n_hist,
+                          const qsmd_event* events, uint64_t n_events,
+                          const uint8_t* pids, uint32_t n_pids, qsmd_wf* out);
+/* Same on device-resident hdr / events / out, enqueued on `stream`. */
+int qsmd_wellformed_batch_device(qsmd_ctx* ctx, const qsmd_hdr* hdr_dev, uint64_t n_hist,
+                                 const qsmd_event* events_dev, uint64_t n_events,
+                                 const uint8_t* pids, uint32_t n_pids, qsmd_wf* out_dev,
+                                 void* stream);
+
 /* Diagnostic: when stamps_dev (device memory, 8 x u64 per stage-0
  * workgroup) is non-NULL, stage 0 runs an instrumented build that records
  * per-workgroup s_memtime totals of its phases (staging, search, output,

@@ -50,6 +50,9 @@ struct qsmd_ctx {
     uint64_t probe_n_hist = 0;
     uint32_t* probe_host = nullptr;    // pinned
     hipEvent_t probe_ev = nullptr;
+    uint8_t* wf_rank_host = nullptr;   // wellformed: pid rank table (pinned) and its device copy
+    char* wf_rank_dev = nullptr;
+    size_t wf_rank_bytes = 0;
     uint64_t split_budget = 4096;      // per-lane node budget before the split stage (0 = none)
     uint64_t stage0_persistent = 0;    // > 0: stage 0 = persistent refill_search (direct) with this grid
     uint64_t refill_min = 8;           // refill kernels: idle lanes before a wavefront refills
@@ -213,6 +216,8 @@ void qsmd_close(qsmd_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->probe_ev) (void)hipEventDestroy(c->probe_ev);
     if (c->probe_host) (void)hipHostFree(c->probe_host);
+    if (c->wf_rank_host) (void)hipHostFree(c->wf_rank_host);
+    if (c->wf_rank_dev) (void)hipFree(c->wf_rank_dev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -687,6 +692,68 @@ int qsmd_check_batch(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, uint64
     HIP_TRY(c, hipMemcpyAsync(&t, d_tot, sizeof t, hipMemcpyDeviceToHost, s), "D2H totals");
     HIP_TRY(c, hipStreamSynchronize(s), "hipStreamSynchronize");
     if (totals_out) *totals_out = t;
+    return QSMD_OK;
+}
+
+static int wellformed_locked(qsmd_ctx* c, const qsmd_hdr* hdr, uint64_t n_hist, const qsmd_event* events,
+                             uint64_t n_events, const uint8_t* pids, uint32_t n_pids, qsmd_wf* out,
+                             hipStream_t s) {
+    if (n_hist && (!hdr || !out)) return fail(c, QSMD_ERR_ARG, "null hdr/out");
+    if (pids && n_pids > QSMD_MAX_PIDS) return fail(c, QSMD_ERR_ARG, "more than 128 pids");
+    // rank table: in the context's pinned buffer, copied in order on the stream
+    if (!c->wf_rank_host &&
+        hipHostMalloc(reinterpret_cast<void**>(&c->wf_rank_host), QSMD_MAX_PIDS, hipHostMallocDefault) != hipSuccess)
+        return fail(c, QSMD_ERR_NOMEM, "hipHostMalloc");
+    HIP_TRY(c, hipStreamSynchronize(s), "hipStreamSynchronize");   // the pinned table may be in flight
+    for (int p = 0; p < QSMD_MAX_PIDS; ++p) c->wf_rank_host[p] = pids ? 0xFF : (uint8_t)p;
+    if (pids)
+        for (uint32_t i = 0; i < n_pids; ++i) {
+            if (pids[i] >= QSMD_MAX_PIDS || c->wf_rank_host[pids[i]] != 0xFF)
+                return fail(c, QSMD_ERR_ARG, "pids: index >= 128 or repeated");
+            c->wf_rank_host[pids[i]] = (uint8_t)i;
+        }
+    int rc = grow(c, &c->wf_rank_dev, &c->wf_rank_bytes, QSMD_MAX_PIDS);
+    if (rc) return rc;
+    HIP_TRY(c, hipMemcpyAsync(c->wf_rank_dev, c->wf_rank_host, QSMD_MAX_PIDS, hipMemcpyHostToDevice, s), "H2D rank");
+    if (!n_hist) return QSMD_OK;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n_hist + 63) / 64, 65536);
+    HIP_TRY(c, launch_wellformed(hdr, n_hist, reinterpret_cast<const uint2*>(events), n_events,
+                                 reinterpret_cast<const uint8_t*>(c->wf_rank_dev), out, grid, s),
+            "wellformed launch");
+    return QSMD_OK;
+}
+
+int qsmd_wellformed_batch_device(qsmd_ctx* c, const qsmd_hdr* hdr_dev, uint64_t n_hist, const qsmd_event* events_dev,
+                                 uint64_t n_events, const uint8_t* pids, uint32_t n_pids, qsmd_wf* out_dev,
+                                 void* stream) {
+    if (!c) return QSMD_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    return wellformed_locked(c, hdr_dev, n_hist, events_dev, n_events, pids, n_pids, out_dev,
+                             stream ? static_cast<hipStream_t>(stream) : c->stream);
+}
+
+int qsmd_wellformed_batch(qsmd_ctx* c, const qsmd_hdr* hdr, uint64_t n_hist, const qsmd_event* events,
+                          uint64_t n_events, const uint8_t* pids, uint32_t n_pids, qsmd_wf* out) {
+    if (!c) return QSMD_ERR_ARG;
+    if (n_hist && (!hdr || !out)) return fail(c, QSMD_ERR_ARG, "null hdr/out");
+    if (n_events && !events) return fail(c, QSMD_ERR_ARG, "null events");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    hipStream_t s = c->stream;
+    const size_t o_ev = align_up(n_hist * sizeof(qsmd_hdr));
+    const size_t o_out = o_ev + align_up(n_events * sizeof(qsmd_event));
+    int rc = grow(c, &c->io, &c->io_bytes, o_out + align_up(n_hist * sizeof(qsmd_wf)));
+    if (rc) return rc;
+    auto* d_hdr = reinterpret_cast<qsmd_hdr*>(c->io);
+    auto* d_ev = reinterpret_cast<qsmd_event*>(c->io + o_ev);
+    auto* d_out = reinterpret_cast<qsmd_wf*>(c->io + o_out);
+    if (n_hist) HIP_TRY(c, hipMemcpyAsync(d_hdr, hdr, n_hist * sizeof(qsmd_hdr), hipMemcpyHostToDevice, s), "H2D hdr");
+    if (n_events) HIP_TRY(c, hipMemcpyAsync(d_ev, events, n_events * sizeof(qsmd_event), hipMemcpyHostToDevice, s), "H2D events");
+    rc = wellformed_locked(c, d_hdr, n_hist, d_ev, n_events, pids, n_pids, d_out, s);
+    if (rc) return rc;
+    if (n_hist) HIP_TRY(c, hipMemcpyAsync(out, d_out, n_hist * sizeof(qsmd_wf), hipMemcpyDeviceToHost, s), "D2H out");
+    HIP_TRY(c, hipStreamSynchronize(s), "hipStreamSynchronize");
     return QSMD_OK;
 }
 

@@ -256,6 +256,10 @@ struct GroupArgs {
 
 hipError_t launch_group(const GroupArgs& p, uint32_t grid, hipStream_t s);
 
+// csrc/wellformed.hip; rank[pid] = position of pid in the `pids` list, 0xFF = not listed
+hipError_t launch_wellformed(const qsmd_hdr* hdr, uint64_t n_hist, const uint2* events, uint64_t n_events,
+                             const uint8_t* rank, qsmd_wf* out, uint32_t grid, hipStream_t s);
+
 // Early exit: relaxed agent-scope read (a stale value only delays skipping).
 __device__ __forceinline__ bool beyond_first_fail(const SearchArgs& a, uint32_t h) {
     return a.first_fail && h > __hip_atomic_load(a.first_fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

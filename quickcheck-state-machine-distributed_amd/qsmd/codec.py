@@ -20,7 +20,38 @@ HDR_DTYPE = np.dtype([("ev_off", "<u4"), ("n_ev", "<u2"), ("n_pid", "u1"),
                       ("model_id", "u1"), ("tag", "<u4"), ("reserved", "<u4")])
 EV_DTYPE = np.dtype([("kp", "u1"), ("code", "u1"), ("a", "u1"), ("b", "u1"),
                      ("val", "<i4")])
-assert HDR_DTYPE.itemsize == 16 and EV_DTYPE.itemsize == 8
+WF_DTYPE = np.dtype([("code", "u1"), ("pid", "u1"), ("ev0", "<u2"), ("ev1", "<u2"), ("reserved", "<u2")])
+assert HDR_DTYPE.itemsize == 16 and EV_DTYPE.itemsize == 8 and WF_DTYPE.itemsize == 8
+
+# qsmd_wf.code -> NotSequential constructor (src/Linearisability.hs:97-104)
+WF_KINDS = {1: "FirstEventIsntInvocation", 2: "InvocationFollowedByInvocation",
+            3: "InvocationFollowedByNonMatchingResponse", 4: "ResponseFollowedByResponse",
+            5: "ResponseFollowedByInvocation", 6: "LoneResponse"}
+WF_ENCODE_ERROR = 0xFE
+
+
+def encode_shape(histories):
+    """Only the shape of a batch (pid and kind of every event, payloads
+    dropped) with ONE dense pid map for the whole batch, in first-use order,
+    as `wellformed` needs: the same `pids` list applies to every history.
+    Returns (hdr, events, pid_index dict)."""
+    pid_index = {}
+    hdr = np.zeros(len(histories), dtype=HDR_DTYPE)
+    kps = []
+    off = 0
+    for i, h in enumerate(histories):
+        for pid, (kind, _) in h:
+            q = pid_index.setdefault(pid, len(pid_index))
+            if q >= 128:
+                raise ValueError("more than 128 distinct pids in the batch")
+            kps.append(q | (0x80 if kind == "R" else 0))
+        hdr[i]["ev_off"] = off
+        hdr[i]["n_ev"] = len(h)
+        off += len(h)
+    hdr["n_pid"] = max(len(pid_index), 1)
+    events = np.zeros(off, dtype=EV_DTYPE)
+    events["kp"] = np.array(kps, dtype=np.uint8) if kps else 0
+    return hdr, events, pid_index
 
 MAX_EVENTS = 128
 MAX_PIDS = 128

@@ -64,6 +64,8 @@ EXPORTS = {
     "qsmd_set_stage0_budget": (_I, [_P, _U64]),
     "qsmd_diag_stamps": (_I, [_P, _P]),
     "qsmd_spread_stats": (_I, [_P, _P]),
+    "qsmd_wellformed_batch": (_I, [_P, _P, _U64, _P, _U64, _P, _U32, _P]),
+    "qsmd_wellformed_batch_device": (_I, [_P, _P, _U64, _P, _U64, _P, _U32, _P, _P]),
     "qsmd_check_batch": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P]),
     "qsmd_check_batch_device": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P, _P]),
     "qsmd_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
@@ -256,6 +258,31 @@ class Context:
 
     def set_stage0_budget(self, nodes):
         self._check(self._lib.qsmd_set_stage0_budget(self._h, int(nodes)), "qsmd_set_stage0_budget")
+
+    def wellformed_arrays(self, hdr, events, pids=None):
+        """Batched `wellformed` (include/qsmd.h qsmd_wellformed_batch) on host
+        arrays; pids = dense pid indices in `pids` order, None = all.
+        Returns a codec.WF_DTYPE array."""
+        hdr = np.ascontiguousarray(hdr, dtype=codec.HDR_DTYPE)
+        events = np.ascontiguousarray(events, dtype=codec.EV_DTYPE)
+        out = np.zeros(len(hdr), dtype=codec.WF_DTYPE)
+        pl = None
+        if pids is not None:
+            pl = np.ascontiguousarray(pids, dtype=np.uint8)
+        rc = self._lib.qsmd_wellformed_batch(
+            self._h, _ptr(hdr) if len(hdr) else None, len(hdr), _ptr(events) if len(events) else None,
+            len(events), _ptr(pl) if pl is not None and len(pl) else None,
+            0 if pl is None else len(pl), _ptr(out) if len(hdr) else None)
+        self._check(rc, "qsmd_wellformed_batch")
+        return out
+
+    def wellformed_device(self, hdr_ptr, n_hist, events_ptr, n_events, out_ptr, pids=None, stream=None):
+        """Device-resident batched `wellformed` (async on stream)."""
+        pl = None if pids is None else np.ascontiguousarray(pids, dtype=np.uint8)
+        rc = self._lib.qsmd_wellformed_batch_device(
+            self._h, hdr_ptr, n_hist, events_ptr, n_events, _ptr(pl) if pl is not None and len(pl) else None,
+            0 if pl is None else len(pl), out_ptr, stream)
+        self._check(rc, "qsmd_wellformed_batch_device")
 
     def spread_stats(self):
         """Spread stage of the last call: (histories, tasks, explored nodes,

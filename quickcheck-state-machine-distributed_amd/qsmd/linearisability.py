@@ -25,7 +25,7 @@ from . import codec, device
 from .models import BY_ID, BY_NAME, DeviceModel, EncodeError, ModelError
 
 __all__ = ["linearisable", "linearisable_batch", "trace", "wellformed", "replay_witness",
-           "CheckResult", "NotSequential", "BudgetExceeded"]
+           "CheckResult", "NotSequential", "BudgetExceeded", "wellformed_batch"]
 
 
 class BudgetExceeded(RuntimeError):
@@ -171,6 +171,40 @@ def _is_sequential(history):
         if k0 == "R" and k1 == "R":
             return NotSequential("ResponseFollowedByResponse", (p0, x0, p1, x1))
         return NotSequential("ResponseFollowedByInvocation", (p0, x0, p1, x1))
+
+
+def wellformed_batch(pids, histories, ctx=None):
+    """Batched ``wellformed pids history`` on the GPU (csrc/wellformed.hip,
+    src/Linearisability.hs:130-135, call site test/Bank.hs:281-283): for each
+    history None (``Right ()``) or the first :class:`NotSequential`, checking
+    each pid's subhistory in ``pids`` order.  Same results as
+    :func:`wellformed` one history at a time."""
+    from . import codec, device
+    hdr, events, pid_index = codec.encode_shape(histories)
+    ranks = [pid_index[p] for p in pids if p in pid_index]
+    own = ctx is None
+    if own:
+        ctx = device.Context(0)
+    try:
+        res = ctx.wellformed_arrays(hdr, events, ranks)
+    finally:
+        if own:
+            ctx.close()
+    out = []
+    for h, r in zip(histories, res):
+        code = int(r["code"])
+        if code == 0:
+            out.append(None)
+            continue
+        if code == codec.WF_ENCODE_ERROR:
+            raise ValueError("history not encodable")
+        e0, e1 = h[int(r["ev0"])], h[int(r["ev1"])]
+        kind = codec.WF_KINDS[code]
+        if kind in ("FirstEventIsntInvocation", "LoneResponse"):
+            out.append(NotSequential(kind, (e0[0], e0[1][1])))
+        else:
+            out.append(NotSequential(kind, (e0[0], e0[1][1], e1[0], e1[1][1])))
+    return out
 
 
 def wellformed(pids, history):

@@ -129,3 +129,20 @@ def test_golden_vectors():
 
 def _untuple(x):
     return tuple(_untuple(y) for y in x) if isinstance(x, list) else x
+
+
+def test_wellformed_ref_matches_host_mirror():
+    """oracle/wellformed_ref.py (checker of the device kernel) and the host
+    mirror qsmd.wellformed agree (src/Linearisability.hs:97-135)."""
+    import random
+
+    import histgen
+    import wellformed_ref
+    from qsmd.linearisability import wellformed
+    rng = random.Random(5)
+    for _ in range(3000):
+        h = (histgen.random_history(rng, "bank", rng.randint(0, 20), rng.randint(1, 4)) if rng.random() < 0.5
+             else histgen.wellformed_history(rng, "ticket", rng.randint(0, 8), rng.randint(1, 4)))
+        pids = rng.sample(["p0", "p1", "p2", "p3"], rng.randint(1, 4))
+        err = wellformed(pids, h)
+        assert wellformed_ref.wellformed(pids, h) == (None if err is None else (err.kind, tuple(err.args)))
