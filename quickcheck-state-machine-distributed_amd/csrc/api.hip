@@ -64,6 +64,9 @@ struct qsmd_ctx {
     uint64_t coop_max = 4096;
     uint64_t stage0_kernel = 0;        // 0 = compact_search, 1 = group_search (in-wave sharing)
     uint64_t stage0_dynamic = 0;       // compact_search: groups from a counter (persistent grid)
+    uint64_t stage0w = 1;              // 33..64-event histories in the compact kernel (else stage 1)
+    uint64_t stage0w_budget = 0;       // stage 0w: nodes per history before it goes to coop64 (0 = none)
+    uint64_t coop64_grid = 512;        // coop64: persistent wavefronts over stage 0w's heavy histories
     uint64_t group_grid = 4096;        // group_search: persistent wavefronts (cap)
     uint64_t group_budget = 16;        // group_search: nodes a shared task searches before it may split
     uint64_t share_idle = 16;          // group_search: idle lanes that start sharing
@@ -91,7 +94,8 @@ struct qsmd_ctx {
 
 namespace {
 
-constexpr uint32_t kStage1Grid = 1024;   // list-mode stages: grid-stride
+constexpr uint32_t kStage0wGrid = 1024;  // list-mode stages: grid-stride
+constexpr uint32_t kStage1Grid = 1024;
 constexpr uint32_t kStage2Grid = 1024;
 constexpr uint32_t kRedoGrid = 64;      // exact re-search of spread histories the speculation cap cut
 constexpr uint32_t kSpreadFinalGrid = 64;
@@ -274,6 +278,13 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "stage0_kernel") {
         if (value > 1) return fail(c, QSMD_ERR_ARG, "stage0_kernel: 0 = compact, 1 = group");
         c->stage0_kernel = value;
+    } else if (n == "stage0w") {
+        c->stage0w = value ? 1 : 0;
+    } else if (n == "stage0w_budget") {
+        c->stage0w_budget = value;
+    } else if (n == "coop64_grid") {
+        if (value < 1 || value > 65536) return fail(c, QSMD_ERR_ARG, "coop64_grid in 1..65536");
+        c->coop64_grid = value;
     } else if (n == "stage0_dynamic") {
         c->stage0_dynamic = value ? 1 : 0;
     } else if (n == "group_grid") {
@@ -407,7 +418,12 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const bool split = c->split_budget && (!max_nodes || c->split_budget < max_nodes);
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
     const uint64_t gsp = split ? kCombineGrid : 0;
-    const uint64_t n_part = g0 + g0b + kStage1Grid + kStage2Grid + gsp + gfx;
+    const uint64_t gw0 = c->stage0w ? kStage0wGrid : 0;   // stage 0w: 33..64-event compact
+    // stage 0w over its node budget: coop64 (+ an exact redo when no split takes the capped ones)
+    const bool heavy_w = gw0 && c->stage0w_budget && (!max_nodes || c->stage0w_budget < max_nodes);
+    const uint64_t gwh = heavy_w ? c->coop64_grid + (split ? 0 : kRedoGrid) : 0;
+    const uint64_t gw = gw0 + gwh;
+    const uint64_t n_part = g0 + g0b + gw + kStage1Grid + kStage2Grid + gsp + gfx;
     // counters: [0] stage-1 list, [1] stage-2 list, [2] timed out, [3] unused,
     //           [4] heavy list, [5] heavy queue head, [6] first failing history,
     //           [7] giant list, [8..9] tasks per variant, [10..11] task queue heads
@@ -416,7 +432,10 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const size_t off_l0 = 512;
     const size_t off_l1 = off_l0 + align_up(n_hist * 4 + 4);
     const size_t off_lh = off_l1 + align_up(n_hist * 4 + 4);
-    const size_t off_lg = off_lh + align_up(n_hist * 4 + 4);
+    const size_t off_lw = off_lh + align_up(n_hist * 4 + 4);
+    const size_t off_lwh = off_lw + (gw0 ? align_up(n_hist * 4 + 4) : 0);      // stage 0w heavy
+    const size_t off_lwr = off_lwh + (heavy_w ? align_up(n_hist * 4 + 4) : 0);   // coop64 redo
+    const size_t off_lg = off_lwr + (heavy_w && !split ? align_up(n_hist * 4 + 4) : 0);
     const size_t off_nd = off_lg + (split ? align_up(n_hist * 4 + 4) : 0);   // nodes if the caller has none
     const size_t off_gr = off_nd + (early && !nodes ? align_up(n_hist * 8) : 0);
     const size_t off_tk = off_gr + (split ? align_up(n_hist * sizeof(GiantRec)) : 0);
@@ -578,13 +597,72 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         ar.partials = part + (g0 + g_heavy) * T_N;
         HIP_TRY(c, launch_refill(ar, kRedoGrid, s), "redo launch");
     }
-    // stage 1: histories with 33..64 events
+    // stage 0w: histories with 33..64 events in the compact layout (u64 masks)
+    uint32_t* l1_in = l0;
+    uint32_t* l1_cnt = cnt + 0;
+    if (gw0) {
+        SearchArgs aw = a;
+        aw.list = l0;
+        aw.list_count = cnt + 0;
+        aw.defer_list = reinterpret_cast<uint32_t*>(c->ws + off_lw);
+        aw.defer_count = cnt + 23;
+        aw.partials = part + (g0 + g0b) * T_N;
+        uint32_t* lwh = reinterpret_cast<uint32_t*>(c->ws + off_lwh);
+        if (heavy_w) {                  // over the budget: -> coop64
+            aw.heavy_list = lwh;
+            aw.heavy_count = cnt + 24;
+            aw.stage0_budget = c->stage0w_budget;
+        } else if (split) {             // as stage 0 without a budget: -> split
+            aw.heavy_list = lg;
+            aw.heavy_count = cnt + 7;
+            aw.stage0_budget = c->split_budget;
+        }
+        HIP_TRY(c, launch_compact64(aw, (uint32_t)gw0, s), "stage 0w launch");
+        if (heavy_w) {
+            // one wavefront per heavy history; one that explores more than the
+            // cap goes to the split stage (giants), or to an exact per-lane redo
+            CoopArgs cp{};
+            cp.s = a;
+            cp.s.giant_list = nullptr;
+            cp.s.partials = part + (g0 + g0b + gw0) * T_N;
+            cp.heavy_list = lwh;
+            cp.heavy_count = cnt + 24;
+            cp.next = cnt + 25;
+            cp.budget = c->coop_budget;
+            cp.max_count = 0xFFFFFFFFu;
+            cp.stats = nullptr;
+            if (split) {
+                cp.explore_cap = 64 * c->split_budget;
+                if (max_nodes) cp.explore_cap = std::min<uint64_t>(cp.explore_cap, 16 * max_nodes + 64 * c->coop_budget);
+                cp.redo_list = lg;
+                cp.redo_count = cnt + 7;
+            } else {
+                cp.explore_cap = max_nodes ? 16 * max_nodes + 64 * c->coop_budget : 0;
+                cp.redo_list = reinterpret_cast<uint32_t*>(c->ws + off_lwr);
+                cp.redo_count = cnt + 26;
+            }
+            HIP_TRY(c, launch_coop64(cp, (uint32_t)c->coop64_grid, s), "coop64 launch");
+            if (!split) {
+                SearchArgs ar = a;      // exact per-lane search, no budget
+                ar.giant_list = nullptr;
+                ar.list = cp.redo_list;
+                ar.list_count = cp.redo_count;
+                ar.defer_list = aw.defer_list;      // never written: stage 0w held them
+                ar.defer_count = aw.defer_count;
+                ar.partials = part + (g0 + g0b + gw0 + c->coop64_grid) * T_N;
+                HIP_TRY(c, launch_compact64(ar, kRedoGrid, s), "coop64 redo launch");
+            }
+        }
+        l1_in = aw.defer_list;
+        l1_cnt = aw.defer_count;
+    }
+    // stage 1: histories with 33..64 events (wide values)
     SearchArgs a1 = a;
-    a1.list = l0;
-    a1.list_count = cnt + 0;
+    a1.list = l1_in;
+    a1.list_count = l1_cnt;
     a1.defer_list = l1;
     a1.defer_count = cnt + 1;
-    a1.partials = part + (g0 + g0b) * T_N;
+    a1.partials = part + (g0 + g0b + gw) * T_N;
     HIP_TRY(c, launch_stage(1, a1, kStage1Grid, s), "stage 1 launch");
     // stage 2: up to 128 events / 128 pids
     SearchArgs a2 = a;
@@ -592,12 +670,12 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a2.list_count = cnt + 1;
     a2.defer_list = l0;            // never written: stage 2 holds every valid history
     a2.defer_count = cnt + 3;
-    a2.partials = part + (g0 + g0b + kStage1Grid) * T_N;
+    a2.partials = part + (g0 + g0b + gw + kStage1Grid) * T_N;
     HIP_TRY(c, launch_stage(2, a2, kStage2Grid, s), "stage 2 launch");
     if (split) {
         SplitArgs p{};
         p.s = a;
-        p.s.partials = part + (g0 + g0b + kStage1Grid + kStage2Grid) * T_N;
+        p.s.partials = part + (g0 + g0b + gw + kStage1Grid + kStage2Grid) * T_N;
         p.giant_list = lg;
         p.giant_count = cnt + 7;
         p.giants = reinterpret_cast<GiantRec*>(c->ws + off_gr);
@@ -623,7 +701,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         HIP_TRY(c, launch_combine(p, kCombineGrid, s), "combine launch");
     }
     if (early) {
-        unsigned long long* pf = part + (g0 + g0b + kStage1Grid + kStage2Grid + gsp) * T_N;
+        unsigned long long* pf = part + (g0 + g0b + gw + kStage1Grid + kStage2Grid + gsp) * T_N;
         HIP_TRY(c, launch_early_exit_fixup(status, nodes, n_hist, cnt + 6, pf, (uint32_t)gfx, s), "fixup launch");
         HIP_TRY(c, launch_reduce(pf, gfx, tot, s), "reduce launch");
     } else {

@@ -44,8 +44,8 @@ namespace qsmd {
 
 // Run one lane's search to its end (status), with the early-exit and time
 // limit checks every 1024 iterations.
-template <int MODE, uint32_t MODEL>
-__device__ __forceinline__ int run_search(LaneDFS<MODEL>& dfs, const SearchArgs& a, const uint32_t* evc,
+template <int MODE, class DFS>
+__device__ __forceinline__ int run_search(DFS& dfs, const SearchArgs& a, const uint32_t* evc,
                                           int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t h,
                                           uint64_t t0) {
     int status;
@@ -63,14 +63,18 @@ __device__ __forceinline__ int run_search(LaneDFS<MODEL>& dfs, const SearchArgs&
 // STAMP = diagnostic build: lane 0 accumulates s_memtime deltas of the
 // phases (header+staging, search, output, groups) into a.stamps[block][0..3]
 // and records its residency (realtime start/end, HW_ID, XCC_ID) in [4..7].
-template <uint32_t MODEL, bool STAMP>
-__global__ __launch_bounds__(C_LANES, 4) void compact_search(SearchArgs a) {
+//
+// G64: the same search for histories of 33..64 events (u64 masks, 16 KB of
+// LDS), run in list mode over the histories stage 0 deferred (a.list).
+template <uint32_t MODEL, bool STAMP, class G = G32>
+__global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(SearchArgs a) {
     constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
-    __shared__ uint32_t s_ev[C_MAXEV][C_LANES];
+    using M = typename G::M;
+    __shared__ uint32_t s_ev[G::EV][C_LANES];
     __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
 
     const int lane = threadIdx.x;
-    const uint64_t total = a.n_hist;
+    const uint64_t total = a.list ? (uint64_t)*a.list_count : a.n_hist;
     Counters cnt;
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t user_limit = a.max_nodes ? a.max_nodes : ~0ull;
@@ -87,23 +91,23 @@ __global__ __launch_bounds__(C_LANES, 4) void compact_search(SearchArgs a) {
         if constexpr (STAMP) ts_a = __builtin_amdgcn_s_memtime();
         const uint64_t idx = base + lane;
         const bool active = idx < total;
-        const uint32_t h = (uint32_t)idx;
+        const uint32_t h = active ? (a.list ? a.list[idx] : (uint32_t)idx) : 0u;
         qsmd_hdr H;
         if (active) H = a.hdr[h];
         else H = qsmd_hdr{0, 0, 0, 0, 0, 0};
         const uint32_t n_ev = H.n_ev, n_pid = H.n_pid;
         const bool enc_ok = active && H.model_id == MODEL && n_ev <= QSMD_MAX_EVENTS &&
                             n_pid <= QSMD_MAX_PIDS && (uint64_t)H.ev_off + n_ev <= a.n_events;
-        const bool small = enc_ok && n_ev <= (uint32_t)C_MAXEV && n_pid <= 8u && a.m0_small;
+        const bool small = enc_ok && n_ev <= (uint32_t)G::EV && n_pid <= 8u && a.m0_small;
 
-        Staged s{0u, 0u, 0u, 0u, 0u, true, true, false};
+        StagedT<M> s{0, 0, 0, 0, 0, true, true, false};
         const uint32_t N0 = __builtin_amdgcn_readfirstlane(n_ev);
         const uint32_t off0 = __builtin_amdgcn_readfirstlane(H.ev_off);
         const bool lane_uni = active && small && n_ev == N0 && H.ev_off == off0 + (uint32_t)lane * N0;
         const bool packed = __ballot(!lane_uni) == 0ull && N0 > 0u;
-        if (packed) stage_packed<MODEL>(a, N0, off0, s_ev, lane);
-        else if (small) stage_lane<MODEL>(a, H, s_ev, lane);
-        if (small) finish_lane(s_ev, lane, n_ev, n_pid, s);
+        if (packed) stage_packed<MODEL, G>(a, N0, off0, s_ev, lane);
+        else if (small) stage_lane<MODEL, G>(a, H, s_ev, lane);
+        if (small) finish_lane<G>(s_ev, lane, n_ev, n_pid, s);
         s.ok = s.ok && enc_ok;
 
         const bool defer = enc_ok && (!small || (s.ok && !s.fits));
@@ -126,7 +130,7 @@ __global__ __launch_bounds__(C_LANES, 4) void compact_search(SearchArgs a) {
         }
 
         int status = -1;
-        LaneDFS<MODEL> dfs;
+        LaneDFS<MODEL, G> dfs;
         dfs.depth = 0;
         dfs.nodes = 0;
         bool search = false;
@@ -283,6 +287,14 @@ __global__ __launch_bounds__(C_LANES) void refill_search(SearchArgs a) {
         }
     }
     cnt.flush(a.partials, lane);
+}
+
+hipError_t launch_compact64(const SearchArgs& a, uint32_t grid, hipStream_t s) {
+    if (a.model_id == QSMD_MODEL_BANK)
+        hipLaunchKernelGGL((compact_search<QSMD_MODEL_BANK, false, G64>), dim3(grid), dim3(C_LANES), 0, s, a);
+    else
+        hipLaunchKernelGGL((compact_search<QSMD_MODEL_TICKET, false, G64>), dim3(grid), dim3(C_LANES), 0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_compact(const SearchArgs& a, uint32_t grid, hipStream_t s) {

@@ -46,24 +46,48 @@ namespace {
 constexpr int kPool = 64;          // pending range tasks per wavefront
 constexpr int kRec = 256;          // task records per history
 
-// key digit i (7 bits): hi holds digits 0..8, lo 9..15
-__device__ __forceinline__ void ckey_put(uint64_t& hi, uint64_t& lo, uint32_t i, uint64_t d) {
-    if (i < 9u) hi |= d << (56u - 7u * i);
-    else lo |= d << (56u - 7u * (i - 9u));
-}
-__device__ __forceinline__ bool ckey_less(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
-    return ah < bh || (ah == bh && al < bl);
-}
+// task key: digit i of DB bits, DPW digits per u64 word, compared
+// lexicographically (G32: 16 digits of 7 bits in 2 words; G64: 32 digits of
+// 8 bits in 4 words -- a path digit 2(j+1) reaches 2*EV)
+template <class G>
+struct CKey {
+    static constexpr int NK = G::EV == 32 ? 2 : 4;
+    static constexpr uint32_t DB = G::EV == 32 ? 7u : 8u;
+    static constexpr uint32_t DPW = 64u / DB;
+    uint64_t w[NK];
+    __device__ __forceinline__ void clear(uint64_t v) {
+#pragma unroll
+        for (int q = 0; q < NK; ++q) w[q] = v;
+    }
+    __device__ __forceinline__ void put(uint32_t i, uint64_t d) {
+        const uint32_t k = i / DPW, sh = 64u - DB * (i % DPW + 1u);
+#pragma unroll
+        for (int q = 0; q < NK; ++q)
+            if ((uint32_t)q == k) w[q] |= d << sh;
+    }
+    __device__ __forceinline__ bool less(const CKey& b) const {
+#pragma unroll
+        for (int q = 0; q < NK; ++q)
+            if (w[q] != b.w[q]) return w[q] < b.w[q];
+        return false;
+    }
+    __device__ __forceinline__ bool operator==(const CKey& b) const {
+        bool e = true;
+#pragma unroll
+        for (int q = 0; q < NK; ++q) e = e && w[q] == b.w[q];
+        return e;
+    }
+};
 
-// wave-wide minimum of a 128-bit key (every lane gets it)
-__device__ __forceinline__ void wave_min_key(uint64_t& hi, uint64_t& lo) {
+// wave-wide minimum of a key (every lane gets it)
+template <class K>
+__device__ __forceinline__ void wave_min_key(K& k) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t oh = __shfl_xor(hi, off, 64), ol = __shfl_xor(lo, off, 64);
-        if (ckey_less(oh, ol, hi, lo)) {
-            hi = oh;
-            lo = ol;
-        }
+        K o;
+#pragma unroll
+        for (int q = 0; q < K::NK; ++q) o.w[q] = __shfl_xor(k.w[q], off, 64);
+        if (o.less(k)) k = o;
     }
 }
 
@@ -78,36 +102,64 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
     return x - v;
 }
 
+template <class G>
 struct Pool {              // pending range tasks (LDS)
-    uint32_t cand[kPool];
+    using M = typename G::M;
+    using K = CKey<G>;
+    M cand[kPool];
     uint32_t meta[kPool];  // depth | found << 8
-    uint32_t rem[kPool];
+    M rem[kPool];
     uint32_t model[kPool]; // Bank: ex | neg << 8; Ticket: RS
-    uint32_t stk[4][kPool];
-    uint64_t khi[kPool], klo[kPool];
+    uint32_t stk[G::LEVELS / 4][kPool];
+    uint64_t key[K::NK][kPool];
     int32_t bal[QSMD_BANK_MAX_ACCOUNTS][kPool];
+    __device__ __forceinline__ K get_key(uint32_t e) const {
+        K k;
+#pragma unroll
+        for (int q = 0; q < K::NK; ++q) k.w[q] = key[q][e];
+        return k;
+    }
+    __device__ __forceinline__ void set_key(uint32_t e, const K& k) {
+#pragma unroll
+        for (int q = 0; q < K::NK; ++q) key[q][e] = k.w[q];
+    }
 };
 
+template <class G>
 struct Recs {              // finished tasks of the current history (LDS)
-    uint64_t khi[kRec], klo[kRec];
+    using K = CKey<G>;
+    uint64_t key[K::NK][kRec];
     uint64_t nodes[kRec];
+    __device__ __forceinline__ K get_key(uint32_t e) const {
+        K k;
+#pragma unroll
+        for (int q = 0; q < K::NK; ++q) k.w[q] = key[q][e];
+        return k;
+    }
+    __device__ __forceinline__ void set_key(uint32_t e, const K& k) {
+#pragma unroll
+        for (int q = 0; q < K::NK; ++q) key[q][e] = k.w[q];
+    }
 };
 
 }  // namespace
 
-template <uint32_t MODEL, int MODE>
-__device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, const Staged& s, uint32_t* s_hist,
-                                             int32_t (*s_bal)[C_LANES], Pool& pool, Recs& rec,
-                                             uint8_t* s_path, int lane, uint64_t t0, Counters& cnt);
+template <uint32_t MODEL, int MODE, class G>
+__device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, const StagedT<typename G::M>& s,
+                                             uint32_t* s_hist, int32_t (*s_bal)[C_LANES], Pool<G>& pool,
+                                             Recs<G>& rec, uint8_t* s_path, int lane, uint64_t t0, Counters& cnt);
 
-template <uint32_t MODEL>
+// G: the geometry (G32: <= 32 events, stage 0's heavy histories; G64: <= 64
+// events, stage 0w's)
+template <uint32_t MODEL, class G>
 __global__ __launch_bounds__(C_LANES) void coop_search(CoopArgs p) {
     constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
-    __shared__ uint32_t s_hist[C_MAXEV];
+    using M = typename G::M;
+    __shared__ uint32_t s_hist[G::EV];
     __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
-    __shared__ Pool pool;
-    __shared__ Recs rec;
-    __shared__ uint8_t s_path[16];
+    __shared__ Pool<G> pool;
+    __shared__ Recs<G> rec;
+    __shared__ uint8_t s_path[G::LEVELS];
     const int lane = threadIdx.x;
     const uint64_t t0 = p.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint32_t n_heavy = *p.heavy_count;
@@ -126,33 +178,39 @@ __global__ __launch_bounds__(C_LANES) void coop_search(CoopArgs p) {
         const qsmd_hdr H = p.s.hdr[h];
         if ((uint32_t)lane < H.n_ev) {
             const uint2 x = p.s.events[H.ev_off + lane];
-            s_hist[lane] = compress<MODEL>(x.x, (int32_t)x.y);
+            s_hist[lane] = compress<MODEL, G>(x.x, (int32_t)x.y);
         }
         // paired?  (every lane evaluates the same history; lane 0 writes the pairs)
-        Staged s{0u, 0u, 0u, 0u, 0u, true, true, false};
-        finish_shared(s_hist, lane == 0, H.n_ev, H.n_pid, s);
+        StagedT<M> s{0, 0, 0, 0, 0, true, true, false};
+        finish_shared<G>(s_hist, lane == 0, H.n_ev, H.n_pid, s);
         if (s.paired)
-            coop_history<MODEL, M_PAIRED>(p, h, s, s_hist, s_bal, pool, rec, s_path, lane, t0, cnt);
+            coop_history<MODEL, M_PAIRED, G>(p, h, s, s_hist, s_bal, pool, rec, s_path, lane, t0, cnt);
         else
-            coop_history<MODEL, M_GENERAL>(p, h, s, s_hist, s_bal, pool, rec, s_path, lane, t0, cnt);
+            coop_history<MODEL, M_GENERAL, G>(p, h, s, s_hist, s_bal, pool, rec, s_path, lane, t0, cnt);
         next = __shfl(next, 0, 64);
     }
     cnt.flush(p.s.partials, lane);
 }
 
-template <uint32_t MODEL, int MODE>
-__device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, const Staged& s, uint32_t* s_hist,
-                                             int32_t (*s_bal)[C_LANES], Pool& pool, Recs& rec,
-                                             uint8_t* s_path, int lane, uint64_t t0, Counters& cnt) {
+template <uint32_t MODEL, int MODE, class G>
+__device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, const StagedT<typename G::M>& s,
+                                             uint32_t* s_hist, int32_t (*s_bal)[C_LANES], Pool<G>& pool,
+                                             Recs<G>& rec, uint8_t* s_path, int lane, uint64_t t0, Counters& cnt) {
     constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
+    using M = typename G::M;
+    using K = CKey<G>;
+    constexpr uint32_t JM = (uint32_t)G::EV - 1u;
     const SearchArgs& a = p.s;
     const qsmd_hdr H = a.hdr[h];
-    LaneDFS<MODEL> dfs;
+    LaneDFS<MODEL, G> dfs;
     dfs.init(s, a, s_bal, lane);                 // every lane: masks, model0 (the root's state)
     bool busy = lane == 0;                       // lane 0 starts the root task
-    uint64_t khi = 0, klo = 0, limit = p.budget;
+    K key, best;
+    key.clear(0ull);
+    best.clear(~0ull);
+    uint64_t limit = p.budget;
     uint32_t pool_n = 0, rec_n = 0;              // wave-uniform
-    uint64_t best_hi = ~0ull, best_lo = ~0ull, best_nodes = 0, prefix_sum = 0, explored = 0;
+    uint64_t best_nodes = 0, prefix_sum = 0, explored = 0;
     uint32_t best_status = QSMD_STATUS_NONLINEARISABLE, best_depth = 0;
     bool incomplete = false, timed = false, skipped = false;
     uint32_t tick = 0, st_splits = 0, st_nosplit = 0, st_compact = 0, st_tasks = 0;
@@ -164,8 +222,7 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
         const uint32_t k = lane_prefix(m);
         if (done) {
             const uint32_t i = rec_n + k;        // room is kept for every running lane
-            rec.khi[i] = khi;
-            rec.klo[i] = klo;
+            rec.set_key(i, key);
             rec.nodes[i] = nodes;
         }
         rec_n += (uint32_t)__builtin_popcountll(m);
@@ -174,37 +231,35 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
     // fold the records below min(every running / pending key, best decider)
     // into prefix_sum, drop the ones above the best decider
     auto compact = [&]() {
-        uint64_t mh = busy ? khi : ~0ull, ml = busy ? klo : ~0ull;
-        for (uint32_t i = lane; i < pool_n; i += 64)
-            if (ckey_less(pool.khi[i], pool.klo[i], mh, ml)) {
-                mh = pool.khi[i];
-                ml = pool.klo[i];
-            }
-        wave_min_key(mh, ml);
-        if (ckey_less(best_hi, best_lo, mh, ml)) {
-            mh = best_hi;
-            ml = best_lo;
+        K mk;
+        if (busy) mk = key;
+        else mk.clear(~0ull);
+        for (uint32_t i = lane; i < pool_n; i += 64) {
+            const K pk = pool.get_key(i);
+            if (pk.less(mk)) mk = pk;
         }
+        wave_min_key(mk);
+        if (best.less(mk)) mk = best;
         uint32_t kept = 0;
         uint64_t folded = 0;
         for (uint32_t c0 = 0; c0 < rec_n; c0 += 64) {
             const uint32_t i = c0 + lane;
             const bool in = i < rec_n;
-            uint64_t rh = 0, rl = 0, rn = 0;
+            K rk;
+            rk.clear(0ull);
+            uint64_t rn = 0;
             if (in) {
-                rh = rec.khi[i];
-                rl = rec.klo[i];
+                rk = rec.get_key(i);
                 rn = rec.nodes[i];
             }
-            const bool below = in && ckey_less(rh, rl, mh, ml);
-            const bool after = in && ckey_less(best_hi, best_lo, rh, rl);
+            const bool below = in && rk.less(mk);
+            const bool after = in && best.less(rk);
             const bool keep = in && !below && !after;
             folded += below ? rn : 0ull;
             const uint64_t km = __ballot(keep);
             if (keep) {                          // in place, in order (kept <= i)
                 const uint32_t d = kept + lane_prefix(km);
-                rec.khi[d] = rh;
-                rec.klo[d] = rl;
+                rec.set_key(d, rk);
                 rec.nodes[d] = rn;
             }
             kept += (uint32_t)__builtin_popcountll(km);
@@ -224,9 +279,8 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
                 const uint32_t k = lane_prefix(idle);
                 if (!busy && k < take) {
                     const uint32_t e = pool_n - 1u - k;
-                    khi = pool.khi[e];
-                    klo = pool.klo[e];
-                    if (!ckey_less(best_hi, best_lo, khi, klo)) {   // else: after the decider, dropped
+                    key = pool.get_key(e);
+                    if (!best.less(key)) {       // else: after the decider, dropped
                         const uint32_t meta = pool.meta[e];
                         dfs.cand = pool.cand[e];
                         dfs.depth = meta & 0xFFu;
@@ -243,7 +297,7 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
                             dfs.RS = mdl;
                         }
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) dfs.stk.w[q] = pool.stk[q][e];
+                        for (int q = 0; q < G::LEVELS / 4; ++q) dfs.stk.w[q] = pool.stk[q][e];
                         dfs.nodes = 0;
                         limit = p.budget;
                         busy = true;
@@ -258,7 +312,7 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
         int st = -1;
         if (busy) {
             st = dfs.template step<1, MODE>(a, s_hist, s_bal, lane, limit);
-            if (st < 0 && ckey_less(best_hi, best_lo, khi, klo)) st = QSMD_STATUS_SKIPPED;   // cancelled
+            if (st < 0 && best.less(key)) st = QSMD_STATUS_SKIPPED;   // cancelled
         }
         if ((tick & 63u) == 0u) {
             if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
@@ -276,17 +330,17 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
         if (at_budget && hungry) {
             // ranges: the current node's untried candidates (+ the one the
             // budget did not count), then each ancestor level's later ones
-            uint32_t r = dfs.rem;
-            k_ranges = (dfs.cand | (1u << dfs.last_j)) ? 1u : 0u;
+            M r = dfs.rem;
+            k_ranges = (dfs.cand | ((M)1 << dfs.last_j)) ? 1u : 0u;
             for (uint32_t l = dfs.depth; l-- > dfs.base;) {
-                const uint32_t j = dfs.stk.get(l) & 31u;
+                const uint32_t j = dfs.stk.get(l) & JM;
                 if (MODE == M_PAIRED) {
-                    r |= (1u << j) | (1u << c_r(s_hist[j]));
+                    r |= ((M)1 << j) | ((M)1 << c_r<G>(s_hist[j]));
                 } else {
-                    const uint32_t gone = ~r & dfs.same_pid(j);
-                    r |= (1u << (31 - __builtin_clz(gone & dfs.INV))) | (1u << (31 - __builtin_clz(gone & dfs.RESP)));
+                    const M gone = ~r & dfs.same_pid(j);
+                    r |= ((M)1 << m_hibit(gone & dfs.INV)) | ((M)1 << m_hibit(gone & dfs.RESP));
                 }
-                k_ranges += (cands(r, dfs.INV, dfs.RESP) & ~below32(j + 1u)) ? 1u : 0u;
+                k_ranges += (cands(r, dfs.INV, dfs.RESP) & ~mask_below(j + 1u, (M)0)) ? 1u : 0u;
             }
         }
         uint32_t off = 0, tot = 0;
@@ -307,14 +361,14 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
             // emit: entry index pool_n + off + (k_ranges - 1 - i), i = 0 at
             // the deepest level (popped first)
             uint32_t i = 0;
-            auto emit = [&](uint32_t c) {
+            auto emit = [&](M c) {
                 const uint32_t e = pool_n + off + (k_ranges - 1u - i);
                 ++i;
-                uint64_t hi = 0, lo = 0;
-                for (uint32_t d = 0; d < dfs.depth; ++d) ckey_put(hi, lo, d, 2ull * ((dfs.stk.get(d) & 31u) + 1u));
-                ckey_put(hi, lo, dfs.depth, 2ull * __builtin_ctz(c) + 1ull);
-                pool.khi[e] = hi;
-                pool.klo[e] = lo;
+                K k;
+                k.clear(0ull);
+                for (uint32_t d = 0; d < dfs.depth; ++d) k.put(d, 2ull * ((dfs.stk.get(d) & JM) + 1u));
+                k.put(dfs.depth, 2ull * m_ctz(c) + 1ull);
+                pool.set_key(e, k);
                 pool.cand[e] = c;
                 pool.meta[e] = dfs.depth | ((uint32_t)dfs.found << 8);
                 pool.rem[e] = dfs.rem;
@@ -326,19 +380,19 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
                     pool.model[e] = dfs.RS;
                 }
 #pragma unroll
-                for (int q = 0; q < 4; ++q) pool.stk[q][e] = dfs.stk.w[q];
+                for (int q = 0; q < G::LEVELS / 4; ++q) pool.stk[q][e] = dfs.stk.w[q];
             };
-            const uint32_t top = dfs.cand | (1u << dfs.last_j);
+            const M top = dfs.cand | ((M)1 << dfs.last_j);
             if (top) emit(top);
             while (dfs.depth > dfs.base) {
                 const uint32_t j = dfs.template undo<1, MODE>(s_hist, s_bal, lane);
                 dfs.found = 1u;
-                const uint32_t c = cands(dfs.rem, dfs.INV, dfs.RESP) & ~below32(j + 1u);
+                const M c = cands(dfs.rem, dfs.INV, dfs.RESP) & ~mask_below(j + 1u, (M)0);
                 if (c) emit(c);
             }
             split_done = true;
         } else if (at_budget) {
-            dfs.cand |= 1u << dfs.last_j;        // search on
+            dfs.cand |= (M)1 << dfs.last_j;      // search on
             limit += p.budget;
         }
         if (tot && room) {
@@ -356,19 +410,20 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
         st_tasks += (uint32_t)__builtin_popcountll(__ballot(fin));
         record(fin, dfs.nodes);
         if (__ballot(decided)) {
-            uint64_t dh = decided ? khi : ~0ull, dl = decided ? klo : ~0ull;
-            wave_min_key(dh, dl);
-            if (ckey_less(dh, dl, best_hi, best_lo)) {
-                best_hi = dh;
-                best_lo = dl;
-                const bool me = decided && khi == dh && klo == dl;
+            K dk;
+            if (decided) dk = key;
+            else dk.clear(~0ull);
+            wave_min_key(dk);
+            if (dk.less(best)) {
+                best = dk;
+                const bool me = decided && key == dk;
                 const uint64_t mm = __ballot(me);
                 const int w = __builtin_ctzll(mm);
                 best_nodes = __shfl(dfs.nodes, w, 64);
                 best_status = (uint32_t)__shfl(st, w, 64);
                 best_depth = (uint32_t)__shfl(dfs.depth, w, 64);
                 if (me && st == QSMD_STATUS_LINEARISABLE)
-                    for (uint32_t d = 0; d < dfs.depth; ++d) s_path[d] = (uint8_t)(dfs.stk.get(d) & 31u);
+                    for (uint32_t d = 0; d < dfs.depth; ++d) s_path[d] = (uint8_t)(dfs.stk.get(d) & JM);
             }
         }
         if (busy && (fin || st == QSMD_STATUS_SKIPPED)) busy = false;
@@ -386,10 +441,10 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
         status = -1;
     } else {
         uint64_t part = 0;
-        for (uint32_t i = lane; i < rec_n; i += 64)
-            if (ckey_less(rec.khi[i], rec.klo[i], best_hi, best_lo) ||
-                (rec.khi[i] == best_hi && rec.klo[i] == best_lo))
-                part += rec.nodes[i];
+        for (uint32_t i = lane; i < rec_n; i += 64) {
+            const K rk = rec.get_key(i);
+            if (!best.less(rk)) part += rec.nodes[i];
+        }
         nodes = prefix_sum + wave_sum64(part);
         status = (int)best_status;
         if (a.max_nodes && nodes > a.max_nodes) {
@@ -428,9 +483,17 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
 
 hipError_t launch_coop(const CoopArgs& p, uint32_t grid, hipStream_t s) {
     if (p.s.model_id == QSMD_MODEL_BANK)
-        hipLaunchKernelGGL(coop_search<QSMD_MODEL_BANK>, dim3(grid), dim3(C_LANES), 0, s, p);
+        hipLaunchKernelGGL((coop_search<QSMD_MODEL_BANK, G32>), dim3(grid), dim3(C_LANES), 0, s, p);
     else
-        hipLaunchKernelGGL(coop_search<QSMD_MODEL_TICKET>, dim3(grid), dim3(C_LANES), 0, s, p);
+        hipLaunchKernelGGL((coop_search<QSMD_MODEL_TICKET, G32>), dim3(grid), dim3(C_LANES), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_coop64(const CoopArgs& p, uint32_t grid, hipStream_t s) {
+    if (p.s.model_id == QSMD_MODEL_BANK)
+        hipLaunchKernelGGL((coop_search<QSMD_MODEL_BANK, G64>), dim3(grid), dim3(C_LANES), 0, s, p);
+    else
+        hipLaunchKernelGGL((coop_search<QSMD_MODEL_TICKET, G64>), dim3(grid), dim3(C_LANES), 0, s, p);
     return hipGetLastError();
 }
 

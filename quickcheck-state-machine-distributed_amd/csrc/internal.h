@@ -227,6 +227,7 @@ struct CoopArgs {
 };
 
 hipError_t launch_coop(const CoopArgs& p, uint32_t grid, hipStream_t s);
+hipError_t launch_coop64(const CoopArgs& p, uint32_t grid, hipStream_t s);
 
 // ------------------------------------------------------------ group stage
 // Stage 0 with in-wavefront sharing (csrc/group.hip).  Per-wavefront scratch
@@ -274,6 +275,8 @@ hipError_t launch_early_exit_fixup(uint8_t* status, uint64_t* nodes, uint64_t n,
 
 // Stage 0 (csrc/compact.hip): <= 32 events, <= 8 pids, 19-bit values.
 hipError_t launch_compact(const SearchArgs& a, uint32_t grid, hipStream_t s);
+// Stage 0w (csrc/compact.hip, G64): <= 64 events, <= 8 pids, 13/25-bit values, list mode.
+hipError_t launch_compact64(const SearchArgs& a, uint32_t grid, hipStream_t s);
 // Stage 0b (csrc/compact.hip): persistent refill search over the heavy list.
 hipError_t launch_refill(const SearchArgs& a, uint32_t grid, hipStream_t s);
 // Stages 1 and 2 (csrc/search.hip): list mode over the deferred histories.

@@ -31,20 +31,46 @@ constexpr int32_t V19_MIN = -(1 << 18), V19_MAX = (1 << 18) - 1;   // model0 val
 // outside the ranges above: the history goes to stage 1).
 constexpr int32_t IVAL_BITS = 14, RVAL_BITS = 25;
 constexpr uint32_t MARK_BAD = 0x70u, MARK_WIDE = 0x60u;
+// Geometry of a compact stage: <= 32 events (u32 event masks, 16 levels,
+// r 5 bits, invocation values 14 bits) or <= 64 events (u64, 32 levels,
+// r 6 bits, invocation values 13 bits).  Response words are the same.
+struct G32 {
+    using M = uint32_t;
+    static constexpr int EV = 32, RB = 5, IVB = 14, LEVELS = 16;
+};
+struct G64 {
+    using M = uint64_t;
+    static constexpr int EV = 64, RB = 6, IVB = 13, LEVELS = 32;
+};
+
 __device__ __forceinline__ uint32_t c_code(uint32_t w) { return (w >> 4) & 7u; }
 __device__ __forceinline__ uint32_t c_a(uint32_t w) { return (w >> 7) & 7u; }
 __device__ __forceinline__ uint32_t c_b(uint32_t w) { return (w >> 10) & 7u; }
-__device__ __forceinline__ uint32_t c_r(uint32_t w) { return (w >> 13) & 31u; }
-__device__ __forceinline__ int32_t c_ival(uint32_t w) { return (int32_t)w >> (32 - IVAL_BITS); }
+template <class G = G32>
+__device__ __forceinline__ uint32_t c_r(uint32_t w) { return (w >> 13) & ((1u << G::RB) - 1u); }
+template <class G = G32>
+__device__ __forceinline__ int32_t c_ival(uint32_t w) { return (int32_t)w >> (32 - G::IVB); }
 __device__ __forceinline__ int32_t c_rval(uint32_t w) { return (int32_t)w >> (32 - RVAL_BITS); }
 
 __device__ __forceinline__ uint32_t below32(uint32_t r) { return (uint32_t)((1ull << r) - 1ull); }
+
+__device__ __forceinline__ uint64_t below64(uint32_t r) { return r >= 64u ? ~0ull : (1ull << r) - 1ull; }
+__device__ __forceinline__ uint32_t mask_below(uint32_t r, uint32_t) { return below32(r); }
+__device__ __forceinline__ uint64_t mask_below(uint32_t r, uint64_t) { return below64(r); }
+__device__ __forceinline__ uint32_t m_ctz(uint32_t x) { return (uint32_t)__builtin_ctz(x); }
+__device__ __forceinline__ uint32_t m_ctz(uint64_t x) { return (uint32_t)__builtin_ctzll(x); }
+__device__ __forceinline__ uint32_t m_hibit(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
+__device__ __forceinline__ uint32_t m_hibit(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
 
 // candidates: remaining invocations before the first remaining response
 // (takeInvocations, src/Linearisability.hs:25-28); branch-free
 __device__ __forceinline__ uint32_t cands(uint32_t rem, uint32_t INV, uint32_t RESP) {
     const uint32_t R = (uint32_t)__builtin_ctzll((uint64_t)(rem & RESP) | (1ull << 32));
     return rem & INV & below32(R);
+}
+__device__ __forceinline__ uint64_t cands(uint64_t rem, uint64_t INV, uint64_t RESP) {
+    const uint64_t rr = rem & RESP;
+    return rem & INV & (rr ? (rr & (0ull - rr)) - 1ull : ~0ull);
 }
 
 // Expected Bank response constructor of `post` (test/Bank.hs:118-131) as a
@@ -100,13 +126,13 @@ __device__ __forceinline__ bool valid_bits(uint32_t lo) {
 }
 
 // The compressed word of one event, or a marker (MARK_BAD / MARK_WIDE).
-template <uint32_t MODEL>
+template <uint32_t MODEL, class G = G32>
 __device__ __forceinline__ uint32_t compress(uint32_t lo, int32_t val) {
     const bool resp = (lo & 0x80u) != 0u;
     const uint32_t head = (lo & 7u) | ((lo >> 4) & 8u) | ((lo >> 4) & 0x70u);   // pid | resp | code
-    const uint32_t inv = head | ((lo >> 9) & 0x380u) | ((lo >> 14) & 0x1C00u) | ((uint32_t)val << (32 - IVAL_BITS));
+    const uint32_t inv = head | ((lo >> 9) & 0x380u) | ((lo >> 14) & 0x1C00u) | ((uint32_t)val << (32 - G::IVB));
     const uint32_t rsp = head | ((uint32_t)val << (32 - RVAL_BITS));
-    const int32_t half = resp ? (1 << (RVAL_BITS - 1)) : (1 << (IVAL_BITS - 1));
+    const int32_t half = resp ? (1 << (RVAL_BITS - 1)) : (1 << (G::IVB - 1));
     const bool fit = (uint32_t)(val + half) < (uint32_t)(2 * half);
     const uint32_t w = resp ? rsp : inv;
     return !valid_bits<MODEL>(lo) ? MARK_BAD : (fit ? w : MARK_WIDE);
@@ -115,14 +141,25 @@ __device__ __forceinline__ uint32_t compress(uint32_t lo, int32_t val) {
 // The DFS stack: 16 levels x 8 bits in 4 VGPRs.  Selection goes through an
 // empty asm so hipcc keeps it a register select (it otherwise turns the
 // select tree into a scratch-memory indexed load).
-struct Stack16 {
-    uint32_t w[4];
+template <int NW>
+struct StackN {
+    uint32_t w[NW];
     __device__ __forceinline__ uint32_t word(uint32_t d) const {
-        uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3];
-        asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
         const uint32_t k = d >> 2;
-        const uint32_t lo = (k & 1u) ? x1 : x0, hi = (k & 1u) ? x3 : x2;
-        return (k & 2u) ? hi : lo;
+        if constexpr (NW == 4) {
+            uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3];
+            asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+            const uint32_t lo = (k & 1u) ? x1 : x0, hi = (k & 1u) ? x3 : x2;
+            return (k & 2u) ? hi : lo;
+        } else {
+            uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4], x5 = w[5], x6 = w[6], x7 = w[7];
+            asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+            asm volatile("" : "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7));
+            const uint32_t a0 = (k & 1u) ? x1 : x0, a1 = (k & 1u) ? x3 : x2, a2 = (k & 1u) ? x5 : x4,
+                           a3 = (k & 1u) ? x7 : x6;
+            const uint32_t b0 = (k & 2u) ? a1 : a0, b1 = (k & 2u) ? a3 : a2;
+            return (k & 4u) ? b1 : b0;
+        }
     }
     __device__ __forceinline__ uint32_t get(uint32_t d) const {
         return (word(d) >> ((d & 3u) * 8u)) & 0xFFu;
@@ -131,18 +168,21 @@ struct Stack16 {
         const uint32_t k = d >> 2, sh = (d & 3u) * 8u;
         const uint32_t keep = ~(0xFFu << sh), ins = v << sh;
 #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) w[q] = (q == k) ? ((w[q] & keep) | ins) : w[q];
+        for (uint32_t q = 0; q < (uint32_t)NW; ++q) w[q] = (q == k) ? ((w[q] & keep) | ins) : w[q];
     }
 };
+using Stack16 = StackN<4>;
 
-struct Staged {
-    uint32_t INV, RESP, P0, P1, P2;
+template <class M>
+struct StagedT {
+    M INV, RESP, P0, P1, P2;
     bool ok, fits, paired;
 };
+using Staged = StagedT<uint32_t>;
 
 // One lane stages its own history: C_CHUNK loads in flight (index clamped
 // into the history, no exec-masked branches), compress into its LDS column.
-template <uint32_t MODEL>
+template <uint32_t MODEL, class G = G32>
 __device__ __forceinline__ void stage_lane(const SearchArgs& a, const qsmd_hdr& H, uint32_t (*s_ev)[C_LANES],
                                            int lane) {
     const uint32_t n_ev = H.n_ev;
@@ -159,7 +199,7 @@ __device__ __forceinline__ void stage_lane(const SearchArgs& a, const qsmd_hdr& 
         }
 #pragma unroll
         for (uint32_t k = 0; k < (uint32_t)C_CHUNK; ++k)
-            if (c0 + k < n_ev) s_ev[c0 + k][lane] = compress<MODEL>(x[k].x, (int32_t)x[k].y);
+            if (c0 + k < n_ev) s_ev[c0 + k][lane] = compress<MODEL, G>(x[k].x, (int32_t)x[k].y);
     }
 }
 
@@ -170,14 +210,14 @@ __device__ __forceinline__ void stage_lane(const SearchArgs& a, const qsmd_hdr& 
 // to its history's lane column.
 __device__ __forceinline__ uint32_t magic_div(uint32_t N0) { return (uint32_t)(0xFFFFFFFFull / N0) + 1u; }
 
-template <uint32_t MODEL>
+template <uint32_t MODEL, class G = G32>
 __device__ __forceinline__ void stage_packed(const SearchArgs& a, uint32_t N0, uint32_t off0,
                                              uint32_t (*s_ev)[C_LANES], int lane) {
     // history of block event g: exact for g < 2^16 (g * N0 < 2^21 << 2^32)
     const uint32_t mg = magic_div(N0);
     auto put = [&](uint32_t g, uint32_t lo, int32_t val) {
         const uint32_t hh = __umulhi(g, mg);
-        s_ev[g - hh * N0][hh] = compress<MODEL>(lo, val);
+        s_ev[g - hh * N0][hh] = compress<MODEL, G>(lo, val);
     };
     const uint32_t total_ev = 64u * N0;
     if ((off0 & 1u) == 0u) {
@@ -223,35 +263,42 @@ __device__ __forceinline__ void stage_packed(const SearchArgs& a, uint32_t N0, u
 // only candidate of pid p is its first remaining invocation, and its
 // response is the next response of p, so the pair is static).  The pair
 // index is OR-ed into the invocation word (r field).
+template <class G = G32>
 __device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane, uint32_t n_ev, uint32_t n_pid,
-                                            Staged& s) {
-    uint32_t W[C_MAXEV];
-#pragma unroll
-    for (uint32_t e = 0; e < (uint32_t)C_MAXEV; ++e) W[e] = s_ev[e][lane];
+                                            StagedT<typename G::M>& s) {
+    using M = typename G::M;
     uint32_t open = 0u, ps_lo = 0u, ps_hi = 0u, unpaired = 0u, bad = 0u, wide = 0u;
+#pragma unroll 1
+    for (uint32_t c0 = 0; c0 < (uint32_t)G::EV; c0 += 32u) {
+    if (c0 >= n_ev) break;
+    uint32_t W[32];                  // the chunk's words first (the pair ORs below go to earlier words)
 #pragma unroll
-    for (uint32_t e = 0; e < (uint32_t)C_MAXEV; ++e) {
+    for (uint32_t k = 0; k < 32u; ++k) W[k] = s_ev[c0 + k][lane];
+#pragma unroll
+    for (uint32_t k = 0; k < 32u; ++k) {
+        const uint32_t e = c0 + k;
         if (e >= n_ev) break;
-        const uint32_t w = W[e];
-        const uint32_t bit = 1u << e;
+        const uint32_t w = W[k];
+        const M bit = (M)1 << e;
         const uint32_t p = w & 7u, resp = (w >> 3) & 1u, mk = w & 0x78u;
         bad |= ((mk == MARK_BAD) | (p >= n_pid)) ? 1u : 0u;
         wide |= mk == MARK_WIDE ? 1u : 0u;
-        s.RESP |= resp ? bit : 0u;
-        s.INV |= resp ? 0u : bit;
-        s.P0 |= (w & 1u) ? bit : 0u;
-        s.P1 |= (w & 2u) ? bit : 0u;
-        s.P2 |= (w & 4u) ? bit : 0u;
+        s.RESP |= resp ? bit : (M)0;
+        s.INV |= resp ? (M)0 : bit;
+        s.P0 |= (w & 1u) ? bit : (M)0;
+        s.P1 |= (w & 2u) ? bit : (M)0;
+        s.P2 |= (w & 4u) ? bit : (M)0;
         // pairing: ps = event index of the open invocation per pid (8 bits each)
         const uint32_t ob = (open >> p) & 1u, sh = (p & 3u) * 8u;
         const bool hi = p >= 4u;
-        const uint32_t j = ((hi ? ps_hi : ps_lo) >> sh) & 31u;
+        const uint32_t j = ((hi ? ps_hi : ps_lo) >> sh) & (uint32_t)(G::EV - 1);
         unpaired |= resp ? (ob ^ 1u) : ob;
         open ^= (resp ? ob : (ob ^ 1u)) << p;                 // inv opens, its resp closes
         const uint32_t ins = (ps_lo & ~(0xFFu << sh)) | (e << sh), insh = (ps_hi & ~(0xFFu << sh)) | (e << sh);
         ps_lo = (!resp && !hi) ? ins : ps_lo;
         ps_hi = (!resp && hi) ? insh : ps_hi;
         if (resp & ob) atomicOr(&s_ev[j][lane], e << 13);
+    }
     }
     s.ok = bad == 0u;
     s.fits = wide == 0u;
@@ -260,28 +307,28 @@ __device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane,
 
 // finish_lane for a history shared by the wavefront (csrc/coop.hip): every
 // lane derives the same masks from s_hist[e]; only `writer` ORs the pairs in.
+template <class G = G32>
 __device__ __forceinline__ void finish_shared(uint32_t* s_hist, bool writer, uint32_t n_ev, uint32_t n_pid,
-                                              Staged& s) {
-    uint32_t W[C_MAXEV];
-#pragma unroll
-    for (uint32_t e = 0; e < (uint32_t)C_MAXEV; ++e) W[e] = s_hist[e];
+                                              StagedT<typename G::M>& s) {
+    using M = typename G::M;
+    // s_hist[e] is read at step e; the writer only ORs into earlier words
     uint32_t open = 0u, ps_lo = 0u, ps_hi = 0u, unpaired = 0u, bad = 0u, wide = 0u;
 #pragma unroll
-    for (uint32_t e = 0; e < (uint32_t)C_MAXEV; ++e) {
+    for (uint32_t e = 0; e < (uint32_t)G::EV; ++e) {
         if (e >= n_ev) break;
-        const uint32_t w = W[e];
-        const uint32_t bit = 1u << e;
+        const uint32_t w = s_hist[e];
+        const M bit = (M)1 << e;
         const uint32_t p = w & 7u, resp = (w >> 3) & 1u, mk = w & 0x78u;
         bad |= ((mk == MARK_BAD) | (p >= n_pid)) ? 1u : 0u;
         wide |= mk == MARK_WIDE ? 1u : 0u;
-        s.RESP |= resp ? bit : 0u;
-        s.INV |= resp ? 0u : bit;
-        s.P0 |= (w & 1u) ? bit : 0u;
-        s.P1 |= (w & 2u) ? bit : 0u;
-        s.P2 |= (w & 4u) ? bit : 0u;
+        s.RESP |= resp ? bit : (M)0;
+        s.INV |= resp ? (M)0 : bit;
+        s.P0 |= (w & 1u) ? bit : (M)0;
+        s.P1 |= (w & 2u) ? bit : (M)0;
+        s.P2 |= (w & 4u) ? bit : (M)0;
         const uint32_t ob = (open >> p) & 1u, sh = (p & 3u) * 8u;
         const bool hi = p >= 4u;
-        const uint32_t j = ((hi ? ps_hi : ps_lo) >> sh) & 31u;
+        const uint32_t j = ((hi ? ps_hi : ps_lo) >> sh) & (uint32_t)(G::EV - 1);
         unpaired |= resp ? (ob ^ 1u) : ob;
         open ^= (resp ? ob : (ob ^ 1u)) << p;
         const uint32_t ins = (ps_lo & ~(0xFFu << sh)) | (e << sh), insh = (ps_hi & ~(0xFFu << sh)) | (e << sh);
@@ -306,24 +353,28 @@ __device__ __forceinline__ void finish_shared(uint32_t* s_hist, bool writer, uin
 // or M_LANE (per-lane `paired` flag).
 enum { M_GENERAL = 0, M_PAIRED = 1, M_LANE = 2 };
 
-template <uint32_t MODEL>
+template <uint32_t MODEL, class G = G32>
 struct LaneDFS {
     static constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
-    uint32_t INV, RESP, P0, P1, P2, ALL;
-    uint32_t rem, cand, depth, ex, neg, RS, found;
+    using M = typename G::M;
+    static constexpr uint32_t JM = (uint32_t)G::EV - 1u;   // event index mask of a stack entry
+    static constexpr uint32_t JB = (uint32_t)G::RB;        // stack entry: j | ex_a << JB | ex_b << JB+1
+    M INV, RESP, P0, P1, P2, ALL;
+    M rem, cand;
+    uint32_t depth, ex, neg, RS, found;
     uint32_t base;          // depth of the search root (0; the task depth in split_search)
     bool paired;
     uint32_t last_j;        // candidate of the most recent try (the one a BUDGET return did not count)
     uint64_t nodes;
-    Stack16 stk;
+    StackN<G::LEVELS / 4> stk;
 
     // events whose pid equals the pid of event j (bit-sliced compare)
-    __device__ __forceinline__ uint32_t same_pid(uint32_t j) const {
-        const uint32_t m0 = 0u - ((P0 >> j) & 1u), m1 = 0u - ((P1 >> j) & 1u), m2 = 0u - ((P2 >> j) & 1u);
+    __device__ __forceinline__ M same_pid(uint32_t j) const {
+        const M m0 = (M)0 - ((P0 >> j) & (M)1), m1 = (M)0 - ((P1 >> j) & (M)1), m2 = (M)0 - ((P2 >> j) & (M)1);
         return ~((P0 ^ m0) | (P1 ^ m1) | (P2 ^ m2)) & ALL;
     }
 
-    __device__ __forceinline__ void init(const Staged& s, const SearchArgs& a, int32_t (*s_bal)[C_LANES],
+    __device__ __forceinline__ void init(const StagedT<M>& s, const SearchArgs& a, int32_t (*s_bal)[C_LANES],
                                          int lane) {
         INV = s.INV; RESP = s.RESP; P0 = s.P0; P1 = s.P1; P2 = s.P2;
         ALL = INV | RESP;
@@ -331,7 +382,8 @@ struct LaneDFS {
         cand = cands(rem, INV, RESP);
         depth = 0; found = 0; nodes = 0; RS = 0; base = 0;
         paired = s.paired;
-        stk.w[0] = stk.w[1] = stk.w[2] = stk.w[3] = 0u;
+#pragma unroll
+        for (int q = 0; q < G::LEVELS / 4; ++q) stk.w[q] = 0u;
         ex = a.m0_exists; neg = 0;
         if constexpr (BANK) {
 #pragma unroll
@@ -352,18 +404,18 @@ struct LaneDFS {
     __device__ __forceinline__ uint32_t undo(const uint32_t* evc, int32_t (*s_bal)[C_LANES], int lane) {
         --depth;
         const uint32_t st = stk.get(depth);
-        const uint32_t j = st & 31u;
+        const uint32_t j = st & JM;
         const uint32_t cj = (BANK || MODE != M_GENERAL) ? evc[j * STRIDE] : 0u;
         if (is_paired<MODE>()) {
-            rem |= (1u << j) | (1u << c_r(cj));
+            rem |= ((M)1 << j) | ((M)1 << c_r<G>(cj));
         } else {
-            const uint32_t gone = ~rem & same_pid(j);
-            rem |= (1u << (31 - __builtin_clz(gone & INV))) | (1u << (31 - __builtin_clz(gone & RESP)));
+            const M gone = ~rem & same_pid(j);
+            rem |= ((M)1 << m_hibit(gone & INV)) | ((M)1 << m_hibit(gone & RESP));
         }
         if constexpr (BANK) {
             const uint32_t code = c_code(cj), ia = c_a(cj), ib = c_b(cj);
-            const int32_t m = c_ival(cj);
-            const uint32_t pa = (st >> 5) & 1u, pb = (st >> 6) & 1u;
+            const int32_t m = c_ival<G>(cj);
+            const uint32_t pa = (st >> JB) & 1u, pb = (st >> (JB + 1u)) & 1u;
             const uint32_t tr = code == QSMD_BANK_TRANSFER ? 1u : 0u;
             const int32_t ba = s_bal[ia][lane], bb = s_bal[ib][lane];
             // undo Transfer's deposit on b, then the step on a
@@ -400,29 +452,30 @@ struct LaneDFS {
                 return (!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE;
             // ---- backtrack: restore the parent level exactly
             const uint32_t j = undo<STRIDE, MODE>(evc, s_bal, lane);
-            cand = cands(rem, INV, RESP) & ~below32(j + 1u);
+            cand = cands(rem, INV, RESP) & ~mask_below(j + 1u, (M)0);
             found = 1u;
             if (!cand) return -1;
         }
         // ---- try the next candidate: straight-line, predicated
-        const uint32_t j = (uint32_t)__builtin_ctz(cand);
-        cand &= cand - 1u;
+        const uint32_t j = m_ctz(cand);
+        cand &= cand - (M)1;
         last_j = j;
         const uint32_t cj = evc[j * STRIDE];
-        uint32_t r, pmj = 0u;
+        uint32_t r;
+        M pmj = 0;
         bool has;                              // findResponse => [] : no child
         if (is_paired<MODE>()) {
-            r = c_r(cj);
+            r = c_r<G>(cj);
             has = r != 0u;
         } else {
             pmj = same_pid(j);
-            const uint32_t rr = rem & pmj & RESP;
-            has = rr != 0u;
-            r = (uint32_t)__builtin_ctz(rr | 0x80000000u);
+            const M rr = rem & pmj & RESP;
+            has = rr != (M)0;
+            r = m_ctz(rr | ((M)1 << JM));
         }
         const uint32_t cr = evc[r * STRIDE];
         const uint32_t code = c_code(cj), rc = c_code(cr);
-        const int32_t m = c_ival(cj), rv = c_rval(cr);
+        const int32_t m = c_ival<G>(cj), rv = c_rval(cr);
         // budget before the node is counted (a BUDGET return leaves the state
         // untouched, so the search can go on with a larger limit)
         const bool over = has & (nodes >= limit);
@@ -442,7 +495,7 @@ struct LaneDFS {
             ok = has & !over & inv_ok & (rc == exp) & (!chk | (rv == bal_a));
             // next' (test/Bank.hs:92-101) on a, then Transfer's deposit on b;
             // stored unconditionally (the old values when !ok)
-            stw = j | (ex_a << 5) | (ex_b << 6);
+            stw = j | (ex_a << JB) | (ex_b << (JB + 1u));
             const int32_t sa = (int32_t)((kBankPos >> code) & 1u) - (int32_t)((kBankNeg >> code) & 1u);
             const int32_t na = ex_a ? bal_a + sa * m : (sa != 0 ? m : 0);
             const uint32_t ex1 = ex | ((chk ? 0u : 1u) << ia);
@@ -483,8 +536,8 @@ struct LaneDFS {
         // descend on success
         stk.put(ok ? depth : 64u, stw);
         depth += ok ? 1u : 0u;
-        const uint32_t fi = rem & pmj & INV;
-        const uint32_t rem2 = rem & ~((is_paired<MODE>() ? (1u << j) : (fi & (0u - fi))) | (1u << r));
+        const M fi = rem & pmj & INV;
+        const M rem2 = rem & ~((is_paired<MODE>() ? ((M)1 << j) : (fi & ((M)0 - fi))) | ((M)1 << r));
         rem = ok ? rem2 : rem;
         cand = ok ? cands(rem2, INV, RESP) : cand;
         found = ok ? 0u : found;
@@ -492,7 +545,7 @@ struct LaneDFS {
     }
 
     __device__ __forceinline__ void write_witness(uint8_t* w, uint32_t n_ev) const {
-        for (uint32_t d = 0; d < depth; ++d) w[d] = (uint8_t)(stk.get(d) & 31u);
+        for (uint32_t d = 0; d < depth; ++d) w[d] = (uint8_t)(stk.get(d) & JM);
         if (depth < n_ev) w[depth] = QSMD_WITNESS_END;
     }
 };

@@ -82,19 +82,30 @@ def test_random_any_shape(ctx, model):
 
 
 @pytest.mark.parametrize("n_ev,n_pid", [(40, 3), (64, 6), (96, 4), (128, 8), (60, 20), (128, 100)])
-def test_stage_cascade(ctx, n_ev, n_pid):
-    """Histories beyond stage 0 (32 events / 8 pids) go through stages 1 and 2."""
+@pytest.mark.parametrize("stage0w", ["on", "off", "coop", "no_heavy"])
+def test_stage_cascade(ctx, n_ev, n_pid, stage0w):
+    """Histories beyond stage 0 (32 events / 8 pids) go through stage 0w
+    (<= 64 events, <= 8 pids; over its node budget: coop64; off: straight to
+    stage 1) and stages 1 and 2.  coop: a 4-node budget sends most of them to
+    coop64; no_heavy (the default): stage 0w searches them to the end."""
     rng = random.Random(n_ev * 1000 + n_pid)
-    for model in ("ticket", "bank"):
-        hs = [histgen.wellformed_history(rng, model, n_ev // 2, n_pid, p_pending=0.0)[:n_ev]
-              for _ in range(300)]
-        hs += [histgen.random_history(rng, model, n_ev, n_pid) for _ in range(300)]
-        m = models.BY_NAME[model]
-        b = codec.encode(m, hs)
-        _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
+    ctx.set_param("stage0w", 0 if stage0w == "off" else 1)
+    ctx.set_param("stage0w_budget", {"coop": 4, "on": 256}.get(stage0w, 0))
+    try:
+        for model in ("ticket", "bank"):
+            hs = [histgen.wellformed_history(rng, model, n_ev // 2, n_pid, p_pending=0.0)[:n_ev]
+                  for _ in range(300)]
+            hs += [histgen.random_history(rng, model, n_ev, n_pid) for _ in range(300)]
+            m = models.BY_NAME[model]
+            b = codec.encode(m, hs)
+            _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
+    finally:
+        ctx.set_param("stage0w", 1)
+        ctx.set_param("stage0w_budget", 0)
 
 
-@pytest.mark.parametrize("model,n_ev", [("bank", 32), ("bank", 20), ("ticket", 24), ("ticket", 7)])
+@pytest.mark.parametrize("model,n_ev", [("bank", 32), ("bank", 20), ("ticket", 24), ("ticket", 7),
+                                        ("bank", 48), ("ticket", 64), ("bank", 33)])
 def test_packed_uniform_batches(ctx, model, n_ev):
     """Batches whose histories are packed back to back with one length take the
     coalesced staging path; corrupt some events (encode errors) and widen some
@@ -171,18 +182,23 @@ def test_model0(ctx):
 
 
 def test_budget(ctx):
+    """The caller's max_nodes through every stage: stage-0 budgets 0/5/50
+    (heavy stages), and for 33..64 events stage 0w's budget (0, the default:
+    no heavy stage; 4: coop64 with its exploration cap)."""
     rng = random.Random(5)
     for n_ev in (40, 24):
         hs = [histgen.random_history(rng, "ticket", n_ev, 1) for _ in range(500)]
         b = codec.encode(models.TICKET, hs)
-        for stage0 in (0, 5, 50):
+        for stage0, w_budget in ((0, 0), (5, 0), (50, 0), (0, 4), (0, 256)):
             ctx.set_stage0_budget(stage0)
+            ctx.set_param("stage0w_budget", w_budget)
             try:
-                for budget in (1, 7, 100):
+                for budget in (1, 7, 100, 1000):
                     st, nd, _ = _compare(ctx, models.MODEL_TICKET, b.hdr, b.events, max_nodes=budget)
                     assert (nd <= budget).all()
             finally:
                 ctx.set_stage0_budget(0)
+                ctx.set_param("stage0w_budget", 0)
 
 
 @pytest.mark.parametrize("name,shift", [("bank_4x16_bugs", 0), ("bank_4x16_bugs", 3000),
