@@ -50,13 +50,17 @@ __device__ __forceinline__ int run_search(DFS& dfs, const SearchArgs& a, const u
                                           uint64_t t0) {
     int status;
     uint32_t iter = 0;
-    while ((status = dfs.template step<C_LANES, MODE>(a, evc, s_bal, lane, limit)) < 0) {
-        if (((iter + 1u) & 1023u) == 0u && beyond_first_fail(a, h)) return QSMD_STATUS_SKIPPED;
-        if (time_up(a, t0, iter)) {
-            atomicOr(a.timed_out, 1u);
-            return QSMD_STATUS_BUDGET;
+    do {                                 // one exit (see LaneDFS::step)
+        status = dfs.template step<C_LANES, MODE>(a, evc, s_bal, lane, limit);
+        if (((++iter) & 1023u) == 0u && status < 0) {
+            if (beyond_first_fail(a, h)) {
+                status = QSMD_STATUS_SKIPPED;
+            } else if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
+                atomicOr(a.timed_out, 1u);
+                status = QSMD_STATUS_BUDGET;
+            }
         }
-    }
+    } while (status < 0);
     return status;
 }
 

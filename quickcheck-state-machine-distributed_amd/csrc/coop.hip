@@ -333,7 +333,7 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
             M r = dfs.rem;
             k_ranges = (dfs.cand | ((M)1 << dfs.last_j)) ? 1u : 0u;
             for (uint32_t l = dfs.depth; l-- > dfs.base;) {
-                const uint32_t j = dfs.stk.get(l) & JM;
+                const uint32_t j = dfs.stk.get(l, dfs.depth) & JM;
                 if (MODE == M_PAIRED) {
                     r |= ((M)1 << j) | ((M)1 << c_r<G>(s_hist[j]));
                 } else {
@@ -366,7 +366,7 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
                 ++i;
                 K k;
                 k.clear(0ull);
-                for (uint32_t d = 0; d < dfs.depth; ++d) k.put(d, 2ull * ((dfs.stk.get(d) & JM) + 1u));
+                for (uint32_t d = 0; d < dfs.depth; ++d) k.put(d, 2ull * ((dfs.stk.get(d, dfs.depth) & JM) + 1u));
                 k.put(dfs.depth, 2ull * m_ctz(c) + 1ull);
                 pool.set_key(e, k);
                 pool.cand[e] = c;
@@ -423,7 +423,7 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
                 best_status = (uint32_t)__shfl(st, w, 64);
                 best_depth = (uint32_t)__shfl(dfs.depth, w, 64);
                 if (me && st == QSMD_STATUS_LINEARISABLE)
-                    for (uint32_t d = 0; d < dfs.depth; ++d) s_path[d] = (uint8_t)(dfs.stk.get(d) & JM);
+                    for (uint32_t d = 0; d < dfs.depth; ++d) s_path[d] = (uint8_t)(dfs.stk.get(d, dfs.depth) & JM);
             }
         }
         if (busy && (fin || st == QSMD_STATUS_SKIPPED)) busy = false;

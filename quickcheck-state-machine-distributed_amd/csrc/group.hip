@@ -151,7 +151,7 @@ __device__ __forceinline__ void group_loop(const GroupArgs& p, LaneDFS<MODEL>& d
             const uint32_t e = first + (k - 1u - i);
             ++i;
             uint64_t hi = 0, lo = 0;
-            for (uint32_t d = 0; d < dfs.depth; ++d) gkey_put(hi, lo, d, 2ull * ((dfs.stk.get(d) & 31u) + 1u));
+            for (uint32_t d = 0; d < dfs.depth; ++d) gkey_put(hi, lo, d, 2ull * ((dfs.stk.get(d, dfs.depth) & 31u) + 1u));
             gkey_put(hi, lo, dfs.depth, 2ull * __builtin_ctz(c) + 1ull);
             sc->khi[e] = hi;
             sc->klo[e] = lo;
@@ -183,7 +183,7 @@ __device__ __forceinline__ void group_loop(const GroupArgs& p, LaneDFS<MODEL>& d
         const uint32_t* evc = &s_ev[0][col];
         uint32_t r = dfs.rem, k = (dfs.cand | extra) ? 1u : 0u;
         for (uint32_t l = dfs.depth; l-- > dfs.base;) {
-            const uint32_t j = dfs.stk.get(l) & 31u;
+            const uint32_t j = dfs.stk.get(l, dfs.depth) & 31u;
             if (dfs.template is_paired<MODE>()) {
                 r |= (1u << j) | (1u << c_r(evc[j * C_LANES]));
             } else {
@@ -397,7 +397,7 @@ __device__ __forceinline__ void group_loop(const GroupArgs& p, LaneDFS<MODEL>& d
                     best_status = uni((uint32_t)__shfl(st, w, 64));
                     best_depth = uni((uint32_t)__shfl((int)dfs.depth, w, 64));
                     if (me && st == QSMD_STATUS_LINEARISABLE)
-                        for (uint32_t d = 0; d < dfs.depth; ++d) s_path[d] = (uint8_t)(dfs.stk.get(d) & 31u);
+                        for (uint32_t d = 0; d < dfs.depth; ++d) s_path[d] = (uint8_t)(dfs.stk.get(d, dfs.depth) & 31u);
                 }
             }
             if (mine && (fin || st == QSMD_STATUS_SKIPPED)) busy = false;

@@ -138,14 +138,17 @@ __device__ __forceinline__ uint32_t compress(uint32_t lo, int32_t val) {
     return !valid_bits<MODEL>(lo) ? MARK_BAD : (fit ? w : MARK_WIDE);
 }
 
-// The DFS stack: 16 levels x 8 bits in 4 VGPRs.  Selection goes through an
-// empty asm so hipcc keeps it a register select (it otherwise turns the
-// select tree into a scratch-memory indexed load).
+// The DFS stack: LEVELS entries x 8 bits in NW VGPRs, kept as a shift
+// register -- the top entry is byte 0, a push shifts every word up by one byte
+// (v_alignbit), a pop down -- so push and pop cost one instruction per word
+// and no indexing.  Entry d of a stack of depth n is byte n - 1 - d (get()),
+// used off the hot path only; there the selection goes through an empty asm
+// so hipcc keeps it a register select (it otherwise turns the select tree
+// into a scratch-memory indexed load).
 template <int NW>
 struct StackN {
     uint32_t w[NW];
-    __device__ __forceinline__ uint32_t word(uint32_t d) const {
-        const uint32_t k = d >> 2;
+    __device__ __forceinline__ uint32_t word(uint32_t k) const {
         if constexpr (NW == 4) {
             uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3];
             asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
@@ -161,17 +164,26 @@ struct StackN {
             return (k & 4u) ? b1 : b0;
         }
     }
-    __device__ __forceinline__ uint32_t get(uint32_t d) const {
-        return (word(d) >> ((d & 3u) * 8u)) & 0xFFu;
+    // entry d (from the bottom) of a stack holding n entries
+    __device__ __forceinline__ uint32_t get(uint32_t d, uint32_t n) const {
+        const uint32_t pos = n - 1u - d;
+        return (word(pos >> 2) >> ((pos & 3u) * 8u)) & 0xFFu;
     }
-    __device__ __forceinline__ void put(uint32_t d, uint32_t v) {
-        const uint32_t k = d >> 2, sh = (d & 3u) * 8u;
-        const uint32_t keep = ~(0xFFu << sh), ins = v << sh;
+    __device__ __forceinline__ uint32_t top() const { return w[0] & 0xFFu; }
+    __device__ __forceinline__ void pop() {
 #pragma unroll
-        for (uint32_t q = 0; q < (uint32_t)NW; ++q) w[q] = (q == k) ? ((w[q] & keep) | ins) : w[q];
+        for (int q = 0; q + 1 < NW; ++q) w[q] = __builtin_amdgcn_alignbit(w[q + 1], w[q], 8u);
+        w[NW - 1] >>= 8;
+    }
+    __device__ __forceinline__ void push_if(bool c, uint32_t v) {
+        uint32_t n[NW];
+        n[0] = (w[0] << 8) | v;
+#pragma unroll
+        for (int q = 1; q < NW; ++q) n[q] = __builtin_amdgcn_alignbit(w[q], w[q - 1], 24u);
+#pragma unroll
+        for (int q = 0; q < NW; ++q) w[q] = c ? n[q] : w[q];
     }
 };
-using Stack16 = StackN<4>;
 
 template <class M>
 struct StagedT {
@@ -403,7 +415,8 @@ struct LaneDFS {
     template <int STRIDE, int MODE>
     __device__ __forceinline__ uint32_t undo(const uint32_t* evc, int32_t (*s_bal)[C_LANES], int lane) {
         --depth;
-        const uint32_t st = stk.get(depth);
+        const uint32_t st = stk.top();
+        stk.pop();
         const uint32_t j = st & JM;
         const uint32_t cj = (BANK || MODE != M_GENERAL) ? evc[j * STRIDE] : 0u;
         if (is_paired<MODE>()) {
@@ -427,10 +440,9 @@ struct LaneDFS {
             s_bal[ib][lane] = fb;                  // a no-op unless Transfer
             s_bal[ia][lane] = ra;                  // written last (ia == ib)
             ex = (ex & ~((1u << ia) | (tr << ib))) | (pa << ia) | ((tr & pb) << ib);
-            const int32_t vb = ia == ib ? ra : fb;
-            neg &= ~((1u << ia) | (1u << ib));
-            neg |= ((ra < 0) ? ((ex >> ia) & 1u) : 0u) << ia;
-            neg |= ((vb < 0) ? ((ex >> ib) & 1u) : 0u) << ib;
+            // the parent held the invariant (a step descends only when it
+            // holds, test/Bank.hs:118), so no existing balance was negative
+            neg = 0u;
         } else {
             RS &= ~(1u << depth);
         }
@@ -445,18 +457,29 @@ struct LaneDFS {
     template <int STRIDE, int MODE = M_GENERAL>
     __device__ __forceinline__ int step(const SearchArgs& a, const uint32_t* evc,
                                         int32_t (*s_bal)[C_LANES], int lane, uint64_t limit) {
+        // one exit at the end (no early returns: the state stays in place
+        // across the two halves instead of being copied between paths)
+        int status = -1;
         if (!cand) {
             // no children: a leaf => True (any' []), the root => False (any []);
             // a subtree rooted at depth base > 0 is an inner node of the reference tree
-            if (!found || depth == base)
-                return (!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE;
-            // ---- backtrack: restore the parent level exactly
-            const uint32_t j = undo<STRIDE, MODE>(evc, s_bal, lane);
-            cand = cands(rem, INV, RESP) & ~mask_below(j + 1u, (M)0);
-            found = 1u;
-            if (!cand) return -1;
+            if (!found || depth == base) {
+                status = (!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE;
+            } else {
+                // ---- backtrack: restore the parent level exactly
+                const uint32_t j = undo<STRIDE, MODE>(evc, s_bal, lane);
+                cand = cands(rem, INV, RESP) & ~mask_below(j + 1u, (M)0);
+                found = 1u;
+            }
         }
-        // ---- try the next candidate: straight-line, predicated
+        if (cand) status = try_next<STRIDE, MODE>(a, evc, s_bal, lane, limit);
+        return status;
+    }
+
+    // ---- try the next candidate: straight-line, predicated
+    template <int STRIDE, int MODE>
+    __device__ __forceinline__ int try_next(const SearchArgs& a, const uint32_t* evc,
+                                            int32_t (*s_bal)[C_LANES], int lane, uint64_t limit) {
         const uint32_t j = m_ctz(cand);
         cand &= cand - (M)1;
         last_j = j;
@@ -506,8 +529,8 @@ struct LaneDFS {
             s_bal[ib][lane] = ok ? fb : bal_b;
             const uint32_t ex2 = ex1 | (tr << ib);
             const int32_t va = ia == ib ? fb : na;
-            uint32_t neg2 = neg & ~((1u << ia) | (1u << ib));
-            neg2 |= ((va < 0) ? ((ex2 >> ia) & 1u) : 0u) << ia;
+            // ok => neg == 0 before the step: only a and b can turn negative
+            uint32_t neg2 = ((va < 0) ? ((ex2 >> ia) & 1u) : 0u) << ia;
             neg2 |= ((fb < 0) ? ((ex2 >> ib) & 1u) : 0u) << ib;
             ex = ok ? ex2 : ex;
             neg = ok ? neg2 : neg;
@@ -526,26 +549,24 @@ struct LaneDFS {
             stw = j;
             RS |= ((ok & !tt) ? 1u : 0u) << depth;   // transition: Reset => Just 0
         }
-        // budget, then Map.! (rare exit)
-        if (over | err) {
-            nodes += over ? 0u : 1u;
-            return over ? QSMD_STATUS_BUDGET : QSMD_STATUS_MODEL_ERROR;
-        }
-        nodes += has ? 1u : 0u;
-        found |= has ? 1u : 0u;
-        // descend on success
-        stk.put(ok ? depth : 64u, stw);
+        // counted unless over the budget (a BUDGET return leaves the state as
+        // it was); Map.! ends the search (the state after it is not used)
+        const bool cnt = has & !over;
+        nodes += cnt ? 1u : 0u;
+        found |= cnt ? 1u : 0u;
+        // descend on success (ok implies !over)
+        stk.push_if(ok, stw);
         depth += ok ? 1u : 0u;
         const M fi = rem & pmj & INV;
         const M rem2 = rem & ~((is_paired<MODE>() ? ((M)1 << j) : (fi & ((M)0 - fi))) | ((M)1 << r));
         rem = ok ? rem2 : rem;
         cand = ok ? cands(rem2, INV, RESP) : cand;
         found = ok ? 0u : found;
-        return -1;
+        return over ? QSMD_STATUS_BUDGET : (err ? QSMD_STATUS_MODEL_ERROR : -1);
     }
 
     __device__ __forceinline__ void write_witness(uint8_t* w, uint32_t n_ev) const {
-        for (uint32_t d = 0; d < depth; ++d) w[d] = (uint8_t)(stk.get(d) & JM);
+        for (uint32_t d = 0; d < depth; ++d) w[d] = (uint8_t)(stk.get(d, depth) & JM);
         if (depth < n_ev) w[depth] = QSMD_WITNESS_END;
     }
 };

@@ -95,7 +95,7 @@ __device__ __forceinline__ void for_each_range(const LaneDFS<MODEL>& dfs, const 
     const uint32_t top = dfs.cand | extra;
     if (top) emit(dfs.depth, top, dfs.found);
     for (uint32_t l = dfs.depth; l-- > dfs.base;) {
-        const uint32_t j = dfs.stk.get(l) & 31u;
+        const uint32_t j = dfs.stk.get(l, dfs.depth) & 31u;
         rem |= removed_at(dfs, evc, rem, j);
         const uint32_t c = cands(rem, dfs.INV, dfs.RESP) & ~below32(j + 1u);
         if (c) emit(l, c, 1u);
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(C_LANES) void spread_search(SpreadArgs p) {
         t->nodes = dfs.nodes;
         if (st == QSMD_STATUS_LINEARISABLE) {
             t->wdepth = (uint8_t)dfs.depth;
-            for (uint32_t d = 0; d < dfs.depth; ++d) t->path[d] = (uint8_t)(dfs.stk.get(d) & 31u);
+            for (uint32_t d = 0; d < dfs.depth; ++d) t->path[d] = (uint8_t)(dfs.stk.get(d, dfs.depth) & 31u);
         }
         if (p.explore_cap && dfs.nodes)
             atomicAdd(reinterpret_cast<unsigned long long*>(&p.hist[L.g].explored), dfs.nodes);
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(C_LANES) void spread_search(SpreadArgs p) {
         const bool room = first + k <= p.cap;
         uint32_t i = 0;
         uint8_t path[16];
-        for (uint32_t d = 0; d < 16u; ++d) path[d] = d < dfs.depth ? (uint8_t)(dfs.stk.get(d) & 31u) : 0u;
+        for (uint32_t d = 0; d < 16u; ++d) path[d] = d < dfs.depth ? (uint8_t)(dfs.stk.get(d, dfs.depth) & 31u) : 0u;
         for_each_range(dfs, evc, extra, [&](uint32_t lvl, uint32_t c, uint32_t found) {
             if (first + i < p.cap) {
                 unsigned long long* w = words(p.tasks + first + i);
