@@ -64,6 +64,7 @@ struct qsmd_ctx {
     uint64_t coop_max = 4096;
     uint64_t stage0_kernel = 0;        // 0 = compact_search, 1 = group_search (in-wave sharing)
     uint64_t stage0_dynamic = 0;       // compact_search: groups from a counter (persistent grid)
+    uint64_t rerun_budget = 0;         // stage 0 budget before the lane re-run (stage 0r); 0 = none
     uint64_t stage0w = 1;              // 33..64-event histories in the compact kernel (else stage 1)
     uint64_t stage0w_budget = 0;       // stage 0w: nodes per history before it goes to coop64 (0 = none)
     uint64_t coop64_grid = 512;        // coop64: persistent wavefronts over stage 0w's heavy histories
@@ -94,7 +95,8 @@ struct qsmd_ctx {
 
 namespace {
 
-constexpr uint32_t kStage0wGrid = 1024;  // list-mode stages: grid-stride
+constexpr uint32_t kStage0wGrid = 1024;
+constexpr uint32_t kRerunGrid = 4096;    // stage 0r (list mode, grid-stride)  // list-mode stages: grid-stride
 constexpr uint32_t kStage1Grid = 1024;
 constexpr uint32_t kStage2Grid = 1024;
 constexpr uint32_t kRedoGrid = 64;      // exact re-search of spread histories the speculation cap cut
@@ -278,6 +280,8 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "stage0_kernel") {
         if (value > 1) return fail(c, QSMD_ERR_ARG, "stage0_kernel: 0 = compact, 1 = group");
         c->stage0_kernel = value;
+    } else if (n == "rerun_budget") {
+        c->rerun_budget = value;
     } else if (n == "stage0w") {
         c->stage0w = value ? 1 : 0;
     } else if (n == "stage0w_budget") {
@@ -418,12 +422,19 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const bool split = c->split_budget && (!max_nodes || c->split_budget < max_nodes);
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
     const uint64_t gsp = split ? kCombineGrid : 0;
+    // stage 0r: stage 0 stops every history at rerun_budget nodes (wavefronts
+    // then run as long as that, not as their slowest lane); the ones over it
+    // are searched again from the root, packed, in list mode, with what stage
+    // 0 would otherwise have done (probe, heavy budget, split)
+    const bool rerun = c->rerun_budget && !grp && !persistent && (!max_nodes || c->rerun_budget < max_nodes);
+    const uint64_t gr = rerun ? std::min<uint64_t>(n_groups, kRerunGrid) : 0;
+    const uint64_t g0r = g0 + gr;
     const uint64_t gw0 = c->stage0w ? kStage0wGrid : 0;   // stage 0w: 33..64-event compact
     // stage 0w over its node budget: coop64 (+ an exact redo when no split takes the capped ones)
     const bool heavy_w = gw0 && c->stage0w_budget && (!max_nodes || c->stage0w_budget < max_nodes);
     const uint64_t gwh = heavy_w ? c->coop64_grid + (split ? 0 : kRedoGrid) : 0;
     const uint64_t gw = gw0 + gwh;
-    const uint64_t n_part = g0 + g0b + gw + kStage1Grid + kStage2Grid + gsp + gfx;
+    const uint64_t n_part = g0r + g0b + gw + kStage1Grid + kStage2Grid + gsp + gfx;
     // counters: [0] stage-1 list, [1] stage-2 list, [2] timed out, [3] unused,
     //           [4] heavy list, [5] heavy queue head, [6] first failing history,
     //           [7] giant list, [8..9] tasks per variant, [10..11] task queue heads
@@ -433,7 +444,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const size_t off_l1 = off_l0 + align_up(n_hist * 4 + 4);
     const size_t off_lh = off_l1 + align_up(n_hist * 4 + 4);
     const size_t off_lw = off_lh + align_up(n_hist * 4 + 4);
-    const size_t off_lwh = off_lw + (gw0 ? align_up(n_hist * 4 + 4) : 0);      // stage 0w heavy
+    const size_t off_lr = off_lw + (gw0 ? align_up(n_hist * 4 + 4) : 0);         // stage 0r list
+    const size_t off_lwh = off_lr + (rerun ? align_up(n_hist * 4 + 4) : 0);      // stage 0w heavy
     const size_t off_lwr = off_lwh + (heavy_w ? align_up(n_hist * 4 + 4) : 0);   // coop64 redo
     const size_t off_lg = off_lwr + (heavy_w && !split ? align_up(n_hist * 4 + 4) : 0);
     const size_t off_nd = off_lg + (split ? align_up(n_hist * 4 + 4) : 0);   // nodes if the caller has none
@@ -537,6 +549,19 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             gp.stats = c->group_stats;
             gp.debug = c->group_debug;
             HIP_TRY(c, launch_group(gp, (uint32_t)g0, s), "stage 0 (group) launch");
+        } else if (rerun) {
+            SearchArgs ab = a0;          // stage 0 with the re-run budget
+            ab.probe = nullptr;
+            ab.heavy_list = reinterpret_cast<uint32_t*>(c->ws + off_lr);
+            ab.heavy_count = cnt + 27;
+            ab.stage0_budget = c->rerun_budget;
+            ab.queue_head = c->stage0_dynamic ? cnt + 21 : nullptr;
+            HIP_TRY(c, launch_compact(ab, (uint32_t)g0, s), "stage 0 launch");
+            a0.list = ab.heavy_list;     // stage 0r: the rest as stage 0 would have
+            a0.list_count = ab.heavy_count;
+            a0.stamps = nullptr;
+            a0.partials = part + g0 * T_N;
+            HIP_TRY(c, launch_compact(a0, (uint32_t)gr, s), "stage 0r launch");
         } else {
             a0.queue_head = c->stage0_dynamic ? cnt + 21 : nullptr;
             HIP_TRY(c, launch_compact(a0, (uint32_t)g0, s), "stage 0 launch");
@@ -549,7 +574,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         CoopArgs cp{};
         cp.s = a;
         cp.s.giant_list = nullptr;
-        cp.s.partials = part + g0 * T_N;
+        cp.s.partials = part + g0r * T_N;
         cp.heavy_list = lh;
         cp.heavy_count = cnt + 4;
         cp.next = cnt + 19;
@@ -566,7 +591,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         SpreadArgs sp{};
         sp.s = a;
         sp.s.giant_list = nullptr;      // the spread stage holds every compact history
-        sp.s.partials = part + (g0 + (coop ? c->coop_grid : 0)) * T_N;
+        sp.s.partials = part + (g0r + (coop ? c->coop_grid : 0)) * T_N;
         sp.heavy_list = lh;
         sp.min_count = c->heavy_stage == 2 ? (uint32_t)c->coop_max + 1u : 0u;
         sp.heavy_count = cnt + 4;
@@ -594,7 +619,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         ar.list = reinterpret_cast<uint32_t*>(c->ws + off_sr);
         ar.list_count = cnt + 13;
         ar.queue_head = cnt + 14;
-        ar.partials = part + (g0 + g_heavy) * T_N;
+        ar.partials = part + (g0r + g_heavy) * T_N;
         HIP_TRY(c, launch_refill(ar, kRedoGrid, s), "redo launch");
     }
     // stage 0w: histories with 33..64 events in the compact layout (u64 masks)
@@ -606,7 +631,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         aw.list_count = cnt + 0;
         aw.defer_list = reinterpret_cast<uint32_t*>(c->ws + off_lw);
         aw.defer_count = cnt + 23;
-        aw.partials = part + (g0 + g0b) * T_N;
+        aw.partials = part + (g0r + g0b) * T_N;
         uint32_t* lwh = reinterpret_cast<uint32_t*>(c->ws + off_lwh);
         if (heavy_w) {                  // over the budget: -> coop64
             aw.heavy_list = lwh;
@@ -624,7 +649,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             CoopArgs cp{};
             cp.s = a;
             cp.s.giant_list = nullptr;
-            cp.s.partials = part + (g0 + g0b + gw0) * T_N;
+            cp.s.partials = part + (g0r + g0b + gw0) * T_N;
             cp.heavy_list = lwh;
             cp.heavy_count = cnt + 24;
             cp.next = cnt + 25;
@@ -649,7 +674,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
                 ar.list_count = cp.redo_count;
                 ar.defer_list = aw.defer_list;      // never written: stage 0w held them
                 ar.defer_count = aw.defer_count;
-                ar.partials = part + (g0 + g0b + gw0 + c->coop64_grid) * T_N;
+                ar.partials = part + (g0r + g0b + gw0 + c->coop64_grid) * T_N;
                 HIP_TRY(c, launch_compact64(ar, kRedoGrid, s), "coop64 redo launch");
             }
         }
@@ -662,7 +687,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a1.list_count = l1_cnt;
     a1.defer_list = l1;
     a1.defer_count = cnt + 1;
-    a1.partials = part + (g0 + g0b + gw) * T_N;
+    a1.partials = part + (g0r + g0b + gw) * T_N;
     HIP_TRY(c, launch_stage(1, a1, kStage1Grid, s), "stage 1 launch");
     // stage 2: up to 128 events / 128 pids
     SearchArgs a2 = a;
@@ -670,12 +695,12 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a2.list_count = cnt + 1;
     a2.defer_list = l0;            // never written: stage 2 holds every valid history
     a2.defer_count = cnt + 3;
-    a2.partials = part + (g0 + g0b + gw + kStage1Grid) * T_N;
+    a2.partials = part + (g0r + g0b + gw + kStage1Grid) * T_N;
     HIP_TRY(c, launch_stage(2, a2, kStage2Grid, s), "stage 2 launch");
     if (split) {
         SplitArgs p{};
         p.s = a;
-        p.s.partials = part + (g0 + g0b + gw + kStage1Grid + kStage2Grid) * T_N;
+        p.s.partials = part + (g0r + g0b + gw + kStage1Grid + kStage2Grid) * T_N;
         p.giant_list = lg;
         p.giant_count = cnt + 7;
         p.giants = reinterpret_cast<GiantRec*>(c->ws + off_gr);
@@ -701,7 +726,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         HIP_TRY(c, launch_combine(p, kCombineGrid, s), "combine launch");
     }
     if (early) {
-        unsigned long long* pf = part + (g0 + g0b + gw + kStage1Grid + kStage2Grid + gsp) * T_N;
+        unsigned long long* pf = part + (g0r + g0b + gw + kStage1Grid + kStage2Grid + gsp) * T_N;
         HIP_TRY(c, launch_early_exit_fixup(status, nodes, n_hist, cnt + 6, pf, (uint32_t)gfx, s), "fixup launch");
         HIP_TRY(c, launch_reduce(pf, gfx, tot, s), "reduce launch");
     } else {

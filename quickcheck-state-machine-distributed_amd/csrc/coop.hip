@@ -340,7 +340,7 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
                     const M gone = ~r & dfs.same_pid(j);
                     r |= ((M)1 << m_hibit(gone & dfs.INV)) | ((M)1 << m_hibit(gone & dfs.RESP));
                 }
-                k_ranges += (cands(r, dfs.INV, dfs.RESP) & ~mask_below(j + 1u, (M)0)) ? 1u : 0u;
+                k_ranges += (cands(r, dfs.INV, dfs.RESP) & mask_above(j, (M)0)) ? 1u : 0u;
             }
         }
         uint32_t off = 0, tot = 0;
@@ -387,7 +387,7 @@ __device__ __forceinline__ void coop_history(const CoopArgs& p, uint32_t h, cons
             while (dfs.depth > dfs.base) {
                 const uint32_t j = dfs.template undo<1, MODE>(s_hist, s_bal, lane);
                 dfs.found = 1u;
-                const M c = cands(dfs.rem, dfs.INV, dfs.RESP) & ~mask_below(j + 1u, (M)0);
+                const M c = cands(dfs.rem, dfs.INV, dfs.RESP) & mask_above(j, (M)0);
                 if (c) emit(c);
             }
             split_done = true;

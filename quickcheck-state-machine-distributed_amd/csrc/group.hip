@@ -174,7 +174,7 @@ __device__ __forceinline__ void group_loop(const GroupArgs& p, LaneDFS<MODEL>& d
         while (dfs.depth > dfs.base) {
             const uint32_t j = dfs.template undo<C_LANES, MODE>(evc, s_bal, lane);
             dfs.found = 1u;
-            const uint32_t c = cands(dfs.rem, dfs.INV, dfs.RESP) & ~below32(j + 1u);
+            const uint32_t c = cands(dfs.rem, dfs.INV, dfs.RESP) & mask_above(j, 0u);
             if (c) emit(c);
         }
     };
@@ -190,7 +190,7 @@ __device__ __forceinline__ void group_loop(const GroupArgs& p, LaneDFS<MODEL>& d
                 const uint32_t gone = ~r & dfs.same_pid(j);
                 r |= (1u << (31 - __builtin_clz(gone & dfs.INV))) | (1u << (31 - __builtin_clz(gone & dfs.RESP)));
             }
-            k += (cands(r, dfs.INV, dfs.RESP) & ~below32(j + 1u)) ? 1u : 0u;
+            k += (cands(r, dfs.INV, dfs.RESP) & mask_above(j, 0u)) ? 1u : 0u;
         }
         return k;
     };

@@ -64,14 +64,19 @@ __device__ __forceinline__ uint32_t m_hibit(uint64_t x) { return 63u - (uint32_t
 
 // candidates: remaining invocations before the first remaining response
 // (takeInvocations, src/Linearisability.hs:25-28); branch-free
+// ((rr & -rr) - 1: the bits below the lowest remaining response; all ones
+// when none remains)
 __device__ __forceinline__ uint32_t cands(uint32_t rem, uint32_t INV, uint32_t RESP) {
-    const uint32_t R = (uint32_t)__builtin_ctzll((uint64_t)(rem & RESP) | (1ull << 32));
-    return rem & INV & below32(R);
+    const uint32_t rr = rem & RESP;
+    return rem & INV & ((rr & (0u - rr)) - 1u);
 }
 __device__ __forceinline__ uint64_t cands(uint64_t rem, uint64_t INV, uint64_t RESP) {
     const uint64_t rr = rem & RESP;
-    return rem & INV & (rr ? (rr & (0ull - rr)) - 1ull : ~0ull);
+    return rem & INV & ((rr & (0ull - rr)) - 1ull);
 }
+// the bits above j (j < width)
+__device__ __forceinline__ uint32_t mask_above(uint32_t j, uint32_t) { return ~1u << j; }
+__device__ __forceinline__ uint64_t mask_above(uint32_t j, uint64_t) { return ~1ull << j; }
 
 // Expected Bank response constructor of `post` (test/Bank.hs:118-131) as a
 // table lookup, index = code*4 + ex_a*2 + ge (3 bits per entry):
@@ -459,18 +464,17 @@ struct LaneDFS {
                                         int32_t (*s_bal)[C_LANES], int lane, uint64_t limit) {
         // one exit at the end (no early returns: the state stays in place
         // across the two halves instead of being copied between paths)
-        int status = -1;
-        if (!cand) {
-            // no children: a leaf => True (any' []), the root => False (any []);
-            // a subtree rooted at depth base > 0 is an inner node of the reference tree
-            if (!found || depth == base) {
-                status = (!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE;
-            } else {
-                // ---- backtrack: restore the parent level exactly
-                const uint32_t j = undo<STRIDE, MODE>(evc, s_bal, lane);
-                cand = cands(rem, INV, RESP) & ~mask_below(j + 1u, (M)0);
-                found = 1u;
-            }
+        // no children: a leaf => True (any' []), the root => False (any []);
+        // a subtree rooted at depth base > 0 is an inner node of the reference tree
+        const bool empty = cand == (M)0;
+        const bool term = empty & ((found == 0u) | (depth == base));
+        int status = !term ? -1
+                           : ((!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE);
+        if (empty & !term) {
+            // ---- backtrack: restore the parent level exactly
+            const uint32_t j = undo<STRIDE, MODE>(evc, s_bal, lane);
+            cand = cands(rem, INV, RESP) & mask_above(j, (M)0);
+            found = 1u;
         }
         if (cand) status = try_next<STRIDE, MODE>(a, evc, s_bal, lane, limit);
         return status;

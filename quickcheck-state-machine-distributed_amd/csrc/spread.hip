@@ -97,7 +97,7 @@ __device__ __forceinline__ void for_each_range(const LaneDFS<MODEL>& dfs, const 
     for (uint32_t l = dfs.depth; l-- > dfs.base;) {
         const uint32_t j = dfs.stk.get(l, dfs.depth) & 31u;
         rem |= removed_at(dfs, evc, rem, j);
-        const uint32_t c = cands(rem, dfs.INV, dfs.RESP) & ~below32(j + 1u);
+        const uint32_t c = cands(rem, dfs.INV, dfs.RESP) & mask_above(j, 0u);
         if (c) emit(l, c, 1u);
     }
 }

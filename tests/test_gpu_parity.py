@@ -165,6 +165,23 @@ def test_generated_configs(ctx, name, n, budget, kernel):
         assert (st == codec.STATUS_LIN).all()
 
 
+@pytest.mark.parametrize("name,n", [("ticket_2x10", 20000), ("bank_4x16", 50000), ("bank_4x16_bugs", 50000)])
+@pytest.mark.parametrize("rerun,budget", [(16, 0), (3, 0), (16, 256), (5, 40)])
+def test_rerun_stage(ctx, name, n, rerun, budget):
+    """Stage 0r: stage 0 stops at `rerun` nodes and the histories over it are
+    searched again from the root (packed, list mode), with the stage-0 heavy
+    budget (and the caller's max_nodes: budget 40 < the heavy budget)."""
+    ctx.set_param("rerun_budget", rerun)
+    ctx.set_stage0_budget(budget)
+    try:
+        hdr, ev, _ = gen.generate_config(name, 3, n)
+        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=40 if rerun == 5 else 10**7)
+    finally:
+        ctx.set_param("rerun_budget", 0)
+        ctx.set_stage0_budget(0)
+        ctx.set_param("stage0_auto", 1)
+
+
 def test_model0(ctx):
     rng = random.Random(99)
     hs = [histgen.wellformed_history(rng, "ticket", rng.randint(1, 6), 2) for _ in range(2000)]
