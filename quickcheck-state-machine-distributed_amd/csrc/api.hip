@@ -64,9 +64,16 @@ struct qsmd_ctx {
     uint64_t coop_max = 4096;
     uint64_t stage0_kernel = 0;        // 0 = compact_search, 1 = group_search (in-wave sharing)
     uint64_t stage0_dynamic = 0;       // compact_search: groups from a counter (persistent grid)
+    uint64_t memo_stage = 1;           // heavy histories: the memo stage (exact-count state memo, csrc/memo.hip)
+    uint64_t mt_entries = 128;         // memo stage: table entries per lane (power of two)
+    uint64_t memo_grid = 512;          // memo stage: workgroups (table slots = memo_grid * 64)
+    char* mt = nullptr;                // memo stage tables: [G32 region][G64 region]
+    size_t mt_bytes = 0;
+    uint32_t mt_epoch = 0;
+    unsigned long long* memo_stats = nullptr;   // diagnostic (memo_stats_ptr)
     uint64_t rerun_budget = 0;         // stage 0 budget before the lane re-run (stage 0r); 0 = none
     uint64_t stage0w = 1;              // 33..64-event histories in the compact kernel (else stage 1)
-    uint64_t stage0w_budget = 0;       // stage 0w: nodes per history before it goes to coop64 (0 = none)
+    uint64_t stage0w_budget = 32;      // stage 0w: nodes per history before the memo stage (coop64 without it; 0 = none)
     uint64_t coop64_grid = 512;        // coop64: persistent wavefronts over stage 0w's heavy histories
     uint64_t group_grid = 4096;        // group_search: persistent wavefronts (cap)
     uint64_t group_budget = 16;        // group_search: nodes a shared task searches before it may split
@@ -99,9 +106,11 @@ constexpr uint32_t kStage0wGrid = 1024;
 constexpr uint32_t kRerunGrid = 4096;    // stage 0r (list mode, grid-stride)  // list-mode stages: grid-stride
 constexpr uint32_t kStage1Grid = 1024;
 constexpr uint32_t kStage2Grid = 1024;
+constexpr uint64_t C_LANES_HOST = 64;     // lanes per wavefront (gfx950)
 constexpr uint32_t kRedoGrid = 64;      // exact re-search of spread histories the speculation cap cut
 constexpr uint32_t kSpreadFinalGrid = 64;
-constexpr uint64_t kAutoBudget = 256;    // adaptive cascade: stage-0 budget when long searches are common
+constexpr uint64_t kAutoProbe = 256;     // adaptive cascade: a long search counts more nodes than this
+constexpr uint64_t kAutoBudget = 128;    // ... and the stage-0 budget when long searches are common
 constexpr uint64_t kAutoFrac = 1000;     // ... i.e. at least 1 history in kAutoFrac needs more
 constexpr uint64_t kTimingSlots = 1024;
 constexpr uint32_t kFrontierGrid = 256;  // split stage: one lane per giant history, grid-stride
@@ -216,6 +225,7 @@ void qsmd_close(qsmd_ctx* c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->sx) (void)hipFree(c->sx);
     if (c->spt) (void)hipFree(c->spt);
+    if (c->mt) (void)hipFree(c->mt);
     if (c->memo) (void)hipFree(c->memo);
     if (c->io) (void)hipFree(c->io);
     for (auto e : c->ev)
@@ -280,6 +290,17 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "stage0_kernel") {
         if (value > 1) return fail(c, QSMD_ERR_ARG, "stage0_kernel: 0 = compact, 1 = group");
         c->stage0_kernel = value;
+    } else if (n == "memo_stage") {
+        c->memo_stage = value ? 1 : 0;
+    } else if (n == "memo_lane_entries") {
+        if (value < 2 || value > 65536 || (value & (value - 1)))
+            return fail(c, QSMD_ERR_ARG, "memo_lane_entries: a power of two in 2..65536");
+        c->mt_entries = value;
+    } else if (n == "memo_grid") {
+        if (value < 1 || value > 65536) return fail(c, QSMD_ERR_ARG, "memo_grid in 1..65536");
+        c->memo_grid = value;
+    } else if (n == "memo_stats_ptr") {     // diagnostic: device buffer of 3 x u64 (iterations, hits, inserts)
+        c->memo_stats = reinterpret_cast<unsigned long long*>(value);
     } else if (n == "rerun_budget") {
         c->rerun_budget = value;
     } else if (n == "stage0w") {
@@ -414,10 +435,11 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const bool probe = c->stage0_auto && !grp && !persistent && !c->probe_pending;
     const bool spread = !grp && budget0 && !persistent && (!max_nodes || budget0 < max_nodes);
     const bool grp_redo = grp && max_nodes;
-    const bool coop = spread && c->heavy_stage != 1;
-    const bool use_spread = spread && c->heavy_stage != 0;
-    const uint64_t g_heavy = (coop ? c->coop_grid : 0) + (use_spread ? kSpreadFinalGrid : 0);
-    const uint64_t g0b = spread ? g_heavy + kRedoGrid : (grp_redo ? kRedoGrid : 0);
+    const bool memo0 = spread && c->memo_stage;       // heavy histories -> the memo stage
+    const bool coop = spread && !memo0 && c->heavy_stage != 1;
+    const bool use_spread = spread && !memo0 && c->heavy_stage != 0;
+    const uint64_t g_heavy = memo0 ? c->memo_grid : (coop ? c->coop_grid : 0) + (use_spread ? kSpreadFinalGrid : 0);
+    const uint64_t g0b = spread ? g_heavy + (memo0 ? 0 : kRedoGrid) : (grp_redo ? kRedoGrid : 0);
     const uint64_t gfx = early ? std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), 4096) : 0;
     const bool split = c->split_budget && (!max_nodes || c->split_budget < max_nodes);
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
@@ -432,7 +454,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const uint64_t gw0 = c->stage0w ? kStage0wGrid : 0;   // stage 0w: 33..64-event compact
     // stage 0w over its node budget: coop64 (+ an exact redo when no split takes the capped ones)
     const bool heavy_w = gw0 && c->stage0w_budget && (!max_nodes || c->stage0w_budget < max_nodes);
-    const uint64_t gwh = heavy_w ? c->coop64_grid + (split ? 0 : kRedoGrid) : 0;
+    const bool memo_w = heavy_w && c->memo_stage;
+    const uint64_t gwh = memo_w ? c->memo_grid : heavy_w ? c->coop64_grid + (split ? 0 : kRedoGrid) : 0;
     const uint64_t gw = gw0 + gwh;
     const uint64_t n_part = g0r + g0b + gw + kStage1Grid + kStage2Grid + gsp + gfx;
     // counters: [0] stage-1 list, [1] stage-2 list, [2] timed out, [3] unused,
@@ -467,6 +490,17 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         rc = grow(c, &c->spt, &c->spt_bytes, sp_cap * sizeof(SpreadTask));
         if (rc) return rc;
         HIP_TRY(c, hipMemsetAsync(c->spt, 0, c->spt_bytes, s), "memset spread tasks");
+    }
+    const uint64_t mt_slots = c->memo_grid * C_LANES_HOST * c->mt_entries;
+    const size_t mt_need = (memo0 || memo_w) ? (size_t)mt_slots * (32 + 64) : 0;
+    if (mt_need && c->mt_bytes < mt_need) {
+        rc = grow(c, &c->mt, &c->mt_bytes, mt_need);
+        if (rc) return rc;
+        HIP_TRY(c, hipMemsetAsync(c->mt, 0, c->mt_bytes, s), "memset memo tables");
+    }
+    if (mt_need && ((++c->mt_epoch) & 0xFFFFFFu) == 0u) {   // 24-bit tags wrapped: clear
+        HIP_TRY(c, hipMemsetAsync(c->mt, 0, c->mt_bytes, s), "memset memo tables");
+        ++c->mt_epoch;
     }
     uint32_t* cnt = reinterpret_cast<uint32_t*>(c->ws + off_cnt);
     qsmd_totals* tot = totals ? totals : reinterpret_cast<qsmd_totals*>(c->ws + off_tot);
@@ -513,7 +547,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.stamps = c->stamps;
     if (probe && !spread) {             // no budget this call: count the long searches
         a0.probe = cnt + 22;
-        a0.probe_nodes = kAutoBudget;
+        a0.probe_nodes = kAutoProbe;
     }
     if (spread) {                       // stage 0 -> spread (-> exact redo)
         a0.heavy_list = lh;
@@ -570,6 +604,20 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
     // stage 0b: histories over the stage-0 node budget: one wavefront per
     // history (coop), or the global dynamic split (spread)
+    if (memo0) {
+        MemoArgs mp{};
+        mp.s = a;
+        mp.s.giant_list = nullptr;
+        mp.s.list = lh;
+        mp.s.list_count = cnt + 4;
+        mp.s.partials = part + g0r * T_N;
+        mp.table = reinterpret_cast<uint32_t*>(c->mt);
+        mp.entries = (uint32_t)c->mt_entries;
+        mp.epoch = c->mt_epoch;
+        mp.stats = c->memo_stats;
+        HIP_TRY(c, launch_memo(mp, (uint32_t)c->memo_grid, false, s), "memo launch");
+        c->last_sp_hist = nullptr;
+    }
     if (coop) {
         CoopArgs cp{};
         cp.s = a;
@@ -613,7 +661,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         c->last_sp_count = sp.heavy_count;
         c->last_sp_ad = sp.ad;
     }
-    if (spread || grp_redo) {
+    if ((spread && !memo0) || grp_redo) {
         SearchArgs ar = a;              // exact per-lane search, no split
         ar.giant_list = nullptr;
         ar.list = reinterpret_cast<uint32_t*>(c->ws + off_sr);
@@ -643,7 +691,19 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             aw.stage0_budget = c->split_budget;
         }
         HIP_TRY(c, launch_compact64(aw, (uint32_t)gw0, s), "stage 0w launch");
-        if (heavy_w) {
+        if (memo_w) {
+            MemoArgs mp{};
+            mp.s = a;
+            mp.s.giant_list = nullptr;
+            mp.s.list = lwh;
+            mp.s.list_count = cnt + 24;
+            mp.s.partials = part + (g0r + g0b + gw0) * T_N;
+            mp.table = reinterpret_cast<uint32_t*>(c->mt + (size_t)mt_slots * 32);
+            mp.entries = (uint32_t)c->mt_entries;
+            mp.epoch = c->mt_epoch;
+            mp.stats = c->memo_stats;
+            HIP_TRY(c, launch_memo(mp, (uint32_t)c->memo_grid, true, s), "memo64 launch");
+        } else if (heavy_w) {
             // one wavefront per heavy history; one that explores more than the
             // cap goes to the split stage (giants), or to an exact per-lane redo
             CoopArgs cp{};
@@ -655,7 +715,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             cp.next = cnt + 25;
             cp.budget = c->coop_budget;
             cp.max_count = 0xFFFFFFFFu;
-            cp.stats = nullptr;
+            cp.stats = c->spread_stamps;    // diagnostic counters (spread_stamps_ptr)
             if (split) {
                 cp.explore_cap = 64 * c->split_budget;
                 if (max_nodes) cp.explore_cap = std::min<uint64_t>(cp.explore_cap, 16 * max_nodes + 64 * c->coop_budget);

@@ -229,6 +229,18 @@ struct CoopArgs {
 hipError_t launch_coop(const CoopArgs& p, uint32_t grid, hipStream_t s);
 hipError_t launch_coop64(const CoopArgs& p, uint32_t grid, hipStream_t s);
 
+// memo stage (csrc/memo.hip): per-lane search of a compact stage's heavy
+// histories (s.list / s.list_count) with an exact-count state memo; one
+// private table of `entries` (power of two) entries per lane slot of the grid
+struct MemoArgs {
+    SearchArgs s;
+    uint32_t* table;              // grid * 64 * entries * (8 | 16) u32
+    uint32_t entries;
+    uint32_t epoch;               // this call's tag (24 bits)
+    unsigned long long* stats;    // diagnostic: iterations, hits, inserts (null = off)
+};
+hipError_t launch_memo(const MemoArgs& p, uint32_t grid, bool wide, hipStream_t s);
+
 // ------------------------------------------------------------ group stage
 // Stage 0 with in-wavefront sharing (csrc/group.hip).  Per-wavefront scratch
 // (global memory, touched by its own wavefront only): the task pool and the

@@ -1,0 +1,270 @@
+// memo.hip -- the memo stage: per-lane search with an exact-count state memo
+// (north star (c)), for the histories the compact stages stop at their node
+// budget.
+//
+// The reference (src/Linearisability.hs:52-69) evaluates a subtree
+// `any' (step model') (interleavings es')` that depends only on the state
+// S = (remaining events es', model') (Lemma L1).  Its outcome and its node
+// count are therefore a function of S.  The search stops at the first
+// success (any / && short-circuit up to the root) or the first Map.! error,
+// so any subtree that is searched to its end before the search ends has
+// failed; a later visit to the same S (another interleaving of the same
+// operations reaching the same model) would fail again after counting the
+// same nodes.  The memo stage records, on leaving such a subtree, (S, its
+// node count) and, on entering a state it holds, adds the count and treats
+// the subtree as failed without searching it.  Verdicts, node counts and
+// witnesses stay the reference's exactly (a witness path never passes a
+// failed subtree); only the work changes: 10^4-node Bank histories with
+// injected bugs take ~10^2 explored nodes.
+//
+// Table: one private table per lane (the lane's slot in the grid), T
+// direct-mapped entries in HBM, keyed by the history index and the call's
+// epoch (stale entries never match, nothing is cleared per call) and the
+// full state: remaining-event mask and model (Bank: existing accounts and
+// their balances as i16; Ticket: Just n).  A state outside that encoding
+// (a balance beyond i16, a count beyond u32) is simply not recorded.  One
+// writer and reader per table: plain loads and stores, no atomics.
+#include <hip/hip_runtime.h>
+
+#include "internal.h"
+#include "lane.h"
+
+namespace qsmd {
+
+namespace {
+
+// entry: G32 8 x u32 (32 B), G64 16 x u32 (64 B)
+//   [0] history index  [1] epoch (24 bits) | ex << 24   [2] rem (lo)  [3] count
+//   [4..7] model: Bank 8 x i16 balances (existing accounts, else 0);
+//          Ticket [4] = just | n << 1
+//   G64: [8] rem (hi)
+template <class G>
+struct MemoEntry {
+    static constexpr int W = G::EV == 32 ? 8 : 16;
+};
+
+template <uint32_t MODEL, class G>
+struct MemoKey {
+    uint32_t w1, rem_lo, rem_hi, m[4];
+    uint32_t slot;
+    bool ok;
+};
+
+struct MemoStats {
+    uint64_t iters, hits, inserts;
+};
+
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x7FEB352Du;
+    h ^= h >> 15;
+    h *= 0x846CA68Bu;
+    h ^= h >> 16;
+    return h;
+}
+
+// the key of the lane's current state (the node at depth dfs.depth)
+template <uint32_t MODEL, class G>
+__device__ __forceinline__ MemoKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d, const SearchArgs& a,
+                                                      int32_t (*s_bal)[C_LANES], int lane, uint32_t epoch,
+                                                      uint32_t mask) {
+    MemoKey<MODEL, G> k;
+    k.ok = true;
+    k.rem_lo = (uint32_t)d.rem;
+    k.rem_hi = G::EV == 64 ? (uint32_t)((uint64_t)d.rem >> 32) : 0u;
+    uint32_t ex = 0;
+    if constexpr (MODEL == QSMD_MODEL_BANK) {
+        ex = d.ex;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int32_t b0 = ((ex >> (2 * q)) & 1u) ? s_bal[2 * q][lane] : 0;
+            const int32_t b1 = ((ex >> (2 * q + 1)) & 1u) ? s_bal[2 * q + 1][lane] : 0;
+            k.ok = k.ok && b0 == (int32_t)(int16_t)b0 && b1 == (int32_t)(int16_t)b1;
+            k.m[q] = ((uint32_t)b0 & 0xFFFFu) | ((uint32_t)b1 << 16);
+        }
+    } else {
+        // model after the levels 0 .. depth-1 (the formula of LaneDFS::try_next)
+        const uint32_t just = d.RS ? 1u : a.m0_just;
+        const int32_t n = d.RS ? (int32_t)(d.depth - 1u - (31u - __builtin_clz(d.RS | 1u)))
+                               : (int32_t)a.m0_val[0] + (a.m0_just ? (int32_t)d.depth : 0);
+        k.ok = !just || n == (int32_t)(int16_t)n;
+        k.m[0] = just | (just ? ((uint32_t)n & 0xFFFFu) << 1 : 0u);
+        k.m[1] = k.m[2] = k.m[3] = 0u;
+    }
+    k.w1 = (epoch & 0xFFFFFFu) | (ex << 24);
+    uint32_t h = mix32(k.rem_lo ^ 0x9E3779B9u);
+    h = mix32(h ^ k.rem_hi ^ (k.w1 >> 24));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) h = mix32(h ^ k.m[q]);
+    k.slot = h & mask;
+    return k;
+}
+
+template <uint32_t MODEL, class G>
+__device__ __forceinline__ bool memo_lookup(const uint32_t* tab, const MemoKey<MODEL, G>& k, uint32_t h,
+                                            uint32_t& count) {
+    const uint4* e = reinterpret_cast<const uint4*>(tab + (uint64_t)k.slot * MemoEntry<G>::W);
+    const uint4 x0 = e[0], x1 = e[1];
+    bool hit = x0.x == h && x0.y == k.w1 && x0.z == k.rem_lo && x1.x == k.m[0] && x1.y == k.m[1] &&
+               x1.z == k.m[2] && x1.w == k.m[3];
+    if constexpr (G::EV == 64) hit = hit && e[2].x == k.rem_hi;
+    count = x0.w;
+    return hit;
+}
+
+template <uint32_t MODEL, class G>
+__device__ __forceinline__ void memo_insert(uint32_t* tab, const MemoKey<MODEL, G>& k, uint32_t h, uint32_t count) {
+    uint4* e = reinterpret_cast<uint4*>(tab + (uint64_t)k.slot * MemoEntry<G>::W);
+    e[0] = make_uint4(h, k.w1, k.rem_lo, count);
+    e[1] = make_uint4(k.m[0], k.m[1], k.m[2], k.m[3]);
+    if constexpr (G::EV == 64) e[2] = make_uint4(k.rem_hi, 0u, 0u, 0u);
+}
+
+// One DFS iteration with the memo (LaneDFS::step plus the two hooks).
+// entry: the lane's column of node counts at entry, per level.
+template <uint32_t MODEL, class G, int MODE>
+__device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* evc,
+                                         int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* tab,
+                                         uint32_t h, uint32_t epoch, uint32_t mask, uint64_t* entry, bool& skip,
+                                         MemoStats& ms) {
+    using M = typename G::M;
+    const bool empty = d.cand == (M)0;
+    const bool term = empty & ((d.found == 0u) | (d.depth == d.base));
+    int status = !term ? -1
+                       : ((!d.found && d.depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE);
+    if (empty & !term) {
+        // leaving the node at depth d.depth: its subtree was searched to the end and failed
+        if (!skip) {
+            const uint64_t cnt = d.nodes - entry[(d.depth - 1u) * C_LANES];
+            const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
+            if (k.ok && cnt <= 0xFFFFFFFFull) {
+                memo_insert<MODEL, G>(tab, k, h, (uint32_t)cnt);
+                ++ms.inserts;
+            }
+        }
+        skip = false;
+        const uint32_t j = d.template undo<C_LANES, MODE>(evc, s_bal, lane);
+        d.cand = cands(d.rem, d.INV, d.RESP) & mask_above(j, (M)0);
+        d.found = 1u;
+    }
+    if (d.cand) {
+        const uint32_t dep0 = d.depth;
+        status = d.template try_next<C_LANES, MODE>(a, evc, s_bal, lane, limit);
+        if (d.depth > dep0) {                     // entered a new node
+            entry[dep0 * C_LANES] = d.nodes;
+            const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
+            uint32_t cnt = 0;
+            if (k.ok && memo_lookup<MODEL, G>(tab, k, h, cnt)) {
+                ++ms.hits;
+                if (d.nodes + cnt > limit) {      // the budget falls inside that subtree
+                    d.nodes = limit;
+                    status = QSMD_STATUS_BUDGET;
+                } else {
+                    d.nodes += cnt;               // the subtree's nodes, counted; it failed
+                    d.cand = (M)0;
+                    d.found = 1u;
+                    skip = true;
+                }
+            }
+        }
+    }
+    return status;
+}
+
+}  // namespace
+
+// list mode over a.list (the heavy histories of a compact stage); every
+// history of the list fits geometry G (it was staged there before)
+template <uint32_t MODEL, class G>
+__global__ __launch_bounds__(C_LANES, 2) void memo_search(MemoArgs p) {
+    constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
+    using M = typename G::M;
+    const SearchArgs& a = p.s;
+    __shared__ uint32_t s_ev[G::EV][C_LANES];
+    __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
+    __shared__ uint64_t s_entry[G::LEVELS][C_LANES];
+
+    const int lane = threadIdx.x;
+    const uint64_t total = *a.list_count;
+    Counters cnt;
+    MemoStats ms{0, 0, 0};
+    const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
+    uint32_t* tab = p.table + ((uint64_t)blockIdx.x * C_LANES + (uint64_t)lane) * (uint64_t)p.entries *
+                                  (uint64_t)MemoEntry<G>::W;
+    const uint32_t mask = p.entries - 1u;
+    for (uint64_t base = (uint64_t)blockIdx.x * C_LANES; base < total; base += (uint64_t)gridDim.x * C_LANES) {
+        const uint64_t idx = base + lane;
+        const bool active = idx < total;
+        const uint32_t h = active ? a.list[idx] : 0u;
+        qsmd_hdr H;
+        if (active) H = a.hdr[h];
+        else H = qsmd_hdr{0, 0, 0, 0, 0, 0};
+        StagedT<M> s{0, 0, 0, 0, 0, true, true, false};
+        if (active) {
+            stage_lane<MODEL, G>(a, H, s_ev, lane);
+            finish_lane<G>(s_ev, lane, H.n_ev, H.n_pid, s);
+        }
+        if (!active) continue;
+        int status = -1;
+        LaneDFS<MODEL, G> dfs;
+        dfs.depth = 0;
+        dfs.nodes = 0;
+        bool search = false;
+        if (!s.ok || !s.fits) {
+            status = QSMD_STATUS_ENCODE_ERROR;   // cannot happen: the list came from a compact stage
+        } else if (H.n_ev == 0) {
+            status = QSMD_STATUS_LINEARISABLE;
+        } else if (beyond_first_fail(a, h)) {
+            status = QSMD_STATUS_SKIPPED;
+        } else {
+            dfs.init(s, a, s_bal, lane);
+            search = true;
+        }
+        if (search) {
+            bool skip = false;
+            uint32_t iter = 0;
+            do {
+                status = memo_step<MODEL, G, M_LANE>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, tab, h, p.epoch,
+                                                     mask, &s_entry[0][lane], skip, ms);
+                if (((++iter) & 1023u) == 0u && status < 0) {
+                    if (beyond_first_fail(a, h)) {
+                        status = QSMD_STATUS_SKIPPED;
+                    } else if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
+                        atomicOr(a.timed_out, 1u);
+                        status = QSMD_STATUS_BUDGET;
+                    }
+                }
+            } while (status < 0);
+            ms.iters += iter;
+        }
+        note_failure(a, h, status);
+        a.status[h] = (uint8_t)status;
+        if (a.nodes) a.nodes[h] = dfs.nodes;
+        if (a.witness && status == QSMD_STATUS_LINEARISABLE) dfs.write_witness(a.witness + H.ev_off, H.n_ev);
+        cnt.add(status, dfs.nodes);
+    }
+    cnt.flush(a.partials, lane);
+    if (p.stats) {                               // diagnostic: iterations, hits, inserts
+        const uint64_t i = wave_sum64(ms.iters), hi = wave_sum64(ms.hits), in = wave_sum64(ms.inserts);
+        if (lane == 0) {
+            atomicAdd(p.stats + 0, (unsigned long long)i);
+            atomicAdd(p.stats + 1, (unsigned long long)hi);
+            atomicAdd(p.stats + 2, (unsigned long long)in);
+        }
+    }
+}
+
+hipError_t launch_memo(const MemoArgs& p, uint32_t grid, bool wide, hipStream_t s) {
+    const bool bank = p.s.model_id == QSMD_MODEL_BANK;
+    if (wide) {
+        if (bank) hipLaunchKernelGGL((memo_search<QSMD_MODEL_BANK, G64>), dim3(grid), dim3(C_LANES), 0, s, p);
+        else hipLaunchKernelGGL((memo_search<QSMD_MODEL_TICKET, G64>), dim3(grid), dim3(C_LANES), 0, s, p);
+    } else {
+        if (bank) hipLaunchKernelGGL((memo_search<QSMD_MODEL_BANK, G32>), dim3(grid), dim3(C_LANES), 0, s, p);
+        else hipLaunchKernelGGL((memo_search<QSMD_MODEL_TICKET, G32>), dim3(grid), dim3(C_LANES), 0, s, p);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace qsmd

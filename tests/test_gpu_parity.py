@@ -82,7 +82,7 @@ def test_random_any_shape(ctx, model):
 
 
 @pytest.mark.parametrize("n_ev,n_pid", [(40, 3), (64, 6), (96, 4), (128, 8), (60, 20), (128, 100)])
-@pytest.mark.parametrize("stage0w", ["on", "off", "coop", "no_heavy"])
+@pytest.mark.parametrize("stage0w", ["on", "off", "coop", "memo", "no_heavy"])
 def test_stage_cascade(ctx, n_ev, n_pid, stage0w):
     """Histories beyond stage 0 (32 events / 8 pids) go through stage 0w
     (<= 64 events, <= 8 pids; over its node budget: coop64; off: straight to
@@ -90,7 +90,8 @@ def test_stage_cascade(ctx, n_ev, n_pid, stage0w):
     coop64; no_heavy (the default): stage 0w searches them to the end."""
     rng = random.Random(n_ev * 1000 + n_pid)
     ctx.set_param("stage0w", 0 if stage0w == "off" else 1)
-    ctx.set_param("stage0w_budget", {"coop": 4, "on": 256}.get(stage0w, 0))
+    ctx.set_param("stage0w_budget", {"coop": 4, "memo": 4, "on": 32}.get(stage0w, 0))
+    ctx.set_param("memo_stage", 0 if stage0w == "coop" else 1)
     try:
         for model in ("ticket", "bank"):
             hs = [histgen.wellformed_history(rng, model, n_ev // 2, n_pid, p_pending=0.0)[:n_ev]
@@ -101,7 +102,8 @@ def test_stage_cascade(ctx, n_ev, n_pid, stage0w):
             _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
     finally:
         ctx.set_param("stage0w", 1)
-        ctx.set_param("stage0w_budget", 0)
+        ctx.set_param("stage0w_budget", 32)
+        ctx.set_param("memo_stage", 1)
 
 
 @pytest.mark.parametrize("model,n_ev", [("bank", 32), ("bank", 20), ("ticket", 24), ("ticket", 7),
@@ -182,6 +184,56 @@ def test_rerun_stage(ctx, name, n, rerun, budget):
         ctx.set_param("stage0_auto", 1)
 
 
+MEMO_CASES = [("bank_4x16_bugs", 50000, 64, 0), ("bank_4x16_bugs", 20000, 8, 300), ("bank_4x16", 50000, 16, 0),
+              ("ticket_2x10", 20000, 4, 0), ("bank_6x24", 20000, 16, 0), ("bank_6x24", 20000, 8, 500)]
+
+
+@pytest.mark.parametrize("name,n,budget,max_nodes", MEMO_CASES)
+@pytest.mark.parametrize("entries", [128, 2])
+def test_memo_stage(ctx, name, n, budget, max_nodes, entries):
+    """The memo stage (exact-count state memo): histories over the stage-0
+    (stage-0w for 48 events) budget are searched with subtree counts reused
+    from a per-lane table; verdicts, node counts and witnesses must equal the
+    reference's.  2 entries: constant replacement; max_nodes: the budget
+    falls inside reused subtrees."""
+    ctx.set_param("memo_stage", 1)
+    ctx.set_param("memo_lane_entries", entries)
+    ctx.set_stage0_budget(budget)
+    ctx.set_param("stage0w_budget", budget)
+    try:
+        hdr, ev, _ = gen.generate_config(name, 5, n)
+        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
+    finally:
+        ctx.set_param("memo_lane_entries", 128)
+        ctx.set_stage0_budget(0)
+        ctx.set_param("stage0w_budget", 32)
+        ctx.set_param("stage0_auto", 1)
+
+
+@pytest.mark.parametrize("model", ["ticket", "bank"])
+def test_memo_stage_any_shape(ctx, model):
+    """Unpaired, shared-pid and pending histories (the general DFS mode) and a
+    non-default model0 through the memo stage."""
+    rng = random.Random(77 if model == "ticket" else 78)
+    hs = []
+    for _ in range(4000):
+        if rng.random() < 0.5:
+            hs.append(histgen.random_history(rng, model, rng.randint(8, 32), rng.randint(1, 5)))
+        else:
+            hs.append(histgen.wellformed_history(rng, model, rng.randint(6, 16), rng.randint(1, 5)))
+    m = models.BY_NAME[model]
+    ctx.set_param("memo_stage", 1)
+    ctx.set_stage0_budget(4)
+    try:
+        b = codec.encode(m, hs)
+        _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
+        if model == "ticket":
+            _compare(ctx, m.model_id, b.hdr, b.events, models.TicketModel(1, 0, 3), max_nodes=200000)
+    finally:
+        ctx.set_stage0_budget(0)
+        ctx.set_param("stage0_auto", 1)
+
+
 def test_model0(ctx):
     rng = random.Random(99)
     hs = [histgen.wellformed_history(rng, "ticket", rng.randint(1, 6), 2) for _ in range(2000)]
@@ -200,22 +252,24 @@ def test_model0(ctx):
 
 def test_budget(ctx):
     """The caller's max_nodes through every stage: stage-0 budgets 0/5/50
-    (heavy stages), and for 33..64 events stage 0w's budget (0, the default:
-    no heavy stage; 4: coop64 with its exploration cap)."""
+    (heavy stages), and for 33..64 events stage 0w's budget (32, the default:
+    the memo stage; 4 without the memo stage: coop64 with its exploration cap)."""
     rng = random.Random(5)
     for n_ev in (40, 24):
         hs = [histgen.random_history(rng, "ticket", n_ev, 1) for _ in range(500)]
         b = codec.encode(models.TICKET, hs)
-        for stage0, w_budget in ((0, 0), (5, 0), (50, 0), (0, 4), (0, 256)):
+        for stage0, w_budget, memo in ((0, 0, 1), (5, 0, 1), (50, 0, 0), (0, 4, 0), (0, 4, 1), (0, 256, 1)):
             ctx.set_stage0_budget(stage0)
             ctx.set_param("stage0w_budget", w_budget)
+            ctx.set_param("memo_stage", memo)
             try:
                 for budget in (1, 7, 100, 1000):
                     st, nd, _ = _compare(ctx, models.MODEL_TICKET, b.hdr, b.events, max_nodes=budget)
                     assert (nd <= budget).all()
             finally:
                 ctx.set_stage0_budget(0)
-                ctx.set_param("stage0w_budget", 0)
+                ctx.set_param("stage0w_budget", 32)
+                ctx.set_param("memo_stage", 1)
 
 
 @pytest.mark.parametrize("name,shift", [("bank_4x16_bugs", 0), ("bank_4x16_bugs", 3000),
@@ -322,7 +376,7 @@ def test_value_ranges_and_pairing(ctx, packed):
     _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**6)
 
 
-HEAVY_DEFAULTS = {"stage0_budget": 0, "heavy_stage": 2, "coop_budget": 16, "spread_budget": 128,
+HEAVY_DEFAULTS = {"memo_stage": 0, "stage0_budget": 0, "heavy_stage": 2, "coop_budget": 16, "spread_budget": 128,
                   "spread_cap": 1 << 22, "coop_max": 4096, "stage0_kernel": 0, "group_budget": 16,
                   "share_idle": 16, "share_nodes": 32}
 
@@ -357,7 +411,7 @@ def test_heavy_stage(ctx, name, n, stage, task_budget, cap):
     try:
         _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev)
     finally:
-        _heavy(ctx)
+        _heavy(ctx, memo_stage=1)
 
 
 @pytest.mark.parametrize("model", ["ticket", "bank"])
@@ -384,7 +438,7 @@ def test_heavy_any_shape(ctx, model, stage):
         for max_nodes in (0, 50, 3000):
             _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=max_nodes)
     finally:
-        _heavy(ctx)
+        _heavy(ctx, memo_stage=1)
 
 
 def test_adaptive_cascade(ctx):
