@@ -65,8 +65,8 @@ struct qsmd_ctx {
     uint64_t stage0_kernel = 0;        // 0 = compact_search, 1 = group_search (in-wave sharing)
     uint64_t stage0_dynamic = 0;       // compact_search: groups from a counter (persistent grid)
     uint64_t memo_stage = 1;           // heavy histories: the memo stage (exact-count state memo, csrc/memo.hip)
-    uint64_t mt_entries = 128;         // memo stage: table entries per lane (power of two)
-    uint64_t memo_grid = 512;          // memo stage: workgroups (table slots = memo_grid * 64)
+    uint64_t mt_entries = 256;         // memo stage: table entries per lane (power of two)
+    uint64_t memo_grid = 2048;         // memo stage: workgroups (table slots = memo_grid * 64)
     char* mt = nullptr;                // memo stage tables: [G32 region][G64 region]
     size_t mt_bytes = 0;
     uint32_t mt_epoch = 0;
@@ -110,7 +110,8 @@ constexpr uint64_t C_LANES_HOST = 64;     // lanes per wavefront (gfx950)
 constexpr uint32_t kRedoGrid = 64;      // exact re-search of spread histories the speculation cap cut
 constexpr uint32_t kSpreadFinalGrid = 64;
 constexpr uint64_t kAutoProbe = 256;     // adaptive cascade: a long search counts more nodes than this
-constexpr uint64_t kAutoBudget = 128;    // ... and the stage-0 budget when long searches are common
+constexpr uint64_t kAutoBudget = 64;     // ... and the stage-0 budget when long searches are common
+constexpr uint64_t kQuietBudget = 512;   // ... and outside heavy mode, with the memo stage
 constexpr uint64_t kAutoFrac = 1000;     // ... i.e. at least 1 history in kAutoFrac needs more
 constexpr uint64_t kTimingSlots = 1024;
 constexpr uint32_t kFrontierGrid = 256;  // split stage: one lane per giant history, grid-stride
@@ -428,10 +429,15 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // re-search, kRedoGrid); group_search shares them in-wave instead
     // adaptive cascade: the decision of the last probe that has landed
     if (c->stage0_auto && c->probe_pending && hipEventQuery(c->probe_ev) == hipSuccess) {
-        c->auto_heavy = (uint64_t)c->probe_host[0] * kAutoFrac >= std::max<uint64_t>(c->probe_n_hist, 1);
+        const uint64_t longs = (uint64_t)c->probe_host[0] + c->probe_host[1];
+        c->auto_heavy = longs * kAutoFrac >= std::max<uint64_t>(c->probe_n_hist, 1);
         c->probe_pending = false;
     }
-    const uint64_t budget0 = c->stage0_auto ? (c->auto_heavy ? kAutoBudget : 0) : c->stage0_budget;
+    // (with the memo stage, a call that is not in heavy mode still sends the
+    // histories over the split budget to it: it searches most of them in far
+    // fewer nodes, and hands the rest to the split stage)
+    const uint64_t quiet0 = c->memo_stage ? std::min<uint64_t>(c->split_budget, kQuietBudget) : 0;
+    const uint64_t budget0 = c->stage0_auto ? (c->auto_heavy ? kAutoBudget : quiet0) : c->stage0_budget;
     const bool probe = c->stage0_auto && !grp && !persistent && !c->probe_pending;
     const bool spread = !grp && budget0 && !persistent && (!max_nodes || budget0 < max_nodes);
     const bool grp_redo = grp && max_nodes;
@@ -545,7 +551,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.defer_count = cnt + 0;
     a0.partials = part;
     a0.stamps = c->stamps;
-    if (probe && !spread) {             // no budget this call: count the long searches
+    if (probe && !c->auto_heavy) {      // not in heavy mode: count the long searches
         a0.probe = cnt + 22;
         a0.probe_nodes = kAutoProbe;
     }
@@ -611,6 +617,11 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         mp.s.list = lh;
         mp.s.list_count = cnt + 4;
         mp.s.partials = part + g0r * T_N;
+        if (split) {                    // the ones the memo does not tame: -> split
+            mp.s.giant_list = lg;
+            mp.s.giant_count = cnt + 7;
+            mp.giant_cap = c->split_budget;
+        }
         mp.table = reinterpret_cast<uint32_t*>(c->mt);
         mp.entries = (uint32_t)c->mt_entries;
         mp.epoch = c->mt_epoch;
@@ -794,7 +805,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     }
     HIP_TRY(c, hipEventRecord(evs[2], s), "hipEventRecord");
     if (probe) {                        // heavy mode: the heavy list is the probe
-        HIP_TRY(c, hipMemcpyAsync(c->probe_host, spread ? cnt + 4 : cnt + 22, 4, hipMemcpyDeviceToHost, s),
+        // long searches: finished ones over kAutoProbe nodes + the ones over the budget
+        HIP_TRY(c, hipMemcpyAsync(c->probe_host + 1, cnt + 22, 4, hipMemcpyDeviceToHost, s), "probe read-back");
+        HIP_TRY(c, hipMemcpyAsync(c->probe_host, spread ? cnt + 4 : cnt + 3, 4, hipMemcpyDeviceToHost, s),
                 "probe read-back");
         HIP_TRY(c, hipEventRecord(c->probe_ev, s), "hipEventRecord");
         c->probe_pending = true;

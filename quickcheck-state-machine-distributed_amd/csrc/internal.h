@@ -238,6 +238,7 @@ struct MemoArgs {
     uint32_t entries;
     uint32_t epoch;               // this call's tag (24 bits)
     unsigned long long* stats;    // diagnostic: iterations, hits, inserts (null = off)
+    uint64_t giant_cap;           // > 0: a search past this many iterations goes to s.giant_list
 };
 hipError_t launch_memo(const MemoArgs& p, uint32_t grid, bool wide, hipStream_t s);
 

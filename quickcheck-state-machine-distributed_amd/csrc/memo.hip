@@ -50,6 +50,8 @@ struct MemoKey {
     bool ok;
 };
 
+constexpr int QSMD_STATUS_HANDED_OFF = 0x40;   // internal: past the giant cap
+
 struct MemoStats {
     uint64_t iters, hits, inserts;
 };
@@ -227,7 +229,10 @@ __global__ __launch_bounds__(C_LANES, 2) void memo_search(MemoArgs p) {
             do {
                 status = memo_step<MODEL, G, M_LANE>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, tab, h, p.epoch,
                                                      mask, &s_entry[0][lane], skip, ms);
-                if (((++iter) & 1023u) == 0u && status < 0) {
+                ++iter;
+                if (p.giant_cap && iter >= p.giant_cap && status < 0) {
+                    status = QSMD_STATUS_HANDED_OFF;
+                } else if ((iter & 1023u) == 0u && status < 0) {
                     if (beyond_first_fail(a, h)) {
                         status = QSMD_STATUS_SKIPPED;
                     } else if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
@@ -237,6 +242,10 @@ __global__ __launch_bounds__(C_LANES, 2) void memo_search(MemoArgs p) {
                 }
             } while (status < 0);
             ms.iters += iter;
+        }
+        if (status == QSMD_STATUS_HANDED_OFF) {  // the split stage searches it (exact, from the root)
+            a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
+            continue;
         }
         note_failure(a, h, status);
         a.status[h] = (uint8_t)status;

@@ -210,6 +210,27 @@ def test_memo_stage(ctx, name, n, budget, max_nodes, entries):
         ctx.set_param("stage0_auto", 1)
 
 
+@pytest.mark.parametrize("split_budget", [16, 200])
+def test_memo_stage_handoff(ctx, split_budget):
+    """Memo-stage searches that reach the giant cap (= split budget
+    iterations) go to the split stage and are searched there from the root;
+    also the default cascade outside heavy mode (stage 0 budget = split
+    budget, then the memo stage)."""
+    ctx.set_param("split_budget", split_budget)
+    try:
+        for name, n in (("bank_4x16_bugs", 30000), ("ticket_2x10", 20000), ("bank_6x24", 5000)):
+            hdr, ev, _ = gen.generate_config(name, 9, n)
+            ctx.set_param("stage0_auto", 0)
+            ctx.set_param("stage0_budget", split_budget)
+            _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+            ctx.set_param("stage0_auto", 1)
+            for _ in range(2):
+                _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+    finally:
+        ctx.set_param("split_budget", 4096)
+        ctx.set_param("stage0_auto", 1)
+
+
 @pytest.mark.parametrize("model", ["ticket", "bank"])
 def test_memo_stage_any_shape(ctx, model):
     """Unpaired, shared-pid and pending histories (the general DFS mode) and a
