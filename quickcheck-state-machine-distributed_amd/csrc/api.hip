@@ -104,14 +104,15 @@ namespace {
 
 constexpr uint32_t kStage0wGrid = 1024;
 constexpr uint32_t kRerunGrid = 4096;    // stage 0r (list mode, grid-stride)  // list-mode stages: grid-stride
-constexpr uint32_t kStage1Grid = 1024;
-constexpr uint32_t kStage2Grid = 1024;
+constexpr uint32_t kStage1Grid = 256;   // rare: values beyond the compact encoding
+constexpr uint32_t kStage2Grid = 512;   // 65..128 events / > 8 pids (16 lanes per workgroup)
 constexpr uint64_t C_LANES_HOST = 64;     // lanes per wavefront (gfx950)
 constexpr uint32_t kRedoGrid = 64;      // exact re-search of spread histories the speculation cap cut
 constexpr uint32_t kSpreadFinalGrid = 64;
 constexpr uint64_t kAutoProbe = 256;     // adaptive cascade: a long search counts more nodes than this
 constexpr uint64_t kAutoBudget = 64;     // ... and the stage-0 budget when long searches are common
 constexpr uint64_t kQuietBudget = 512;   // ... and outside heavy mode, with the memo stage
+constexpr uint64_t kQuietMemoGrid = 256; // memo-stage grid outside heavy mode
 constexpr uint64_t kAutoFrac = 1000;     // ... i.e. at least 1 history in kAutoFrac needs more
 constexpr uint64_t kTimingSlots = 1024;
 constexpr uint32_t kFrontierGrid = 256;  // split stage: one lane per giant history, grid-stride
@@ -444,7 +445,11 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const bool memo0 = spread && c->memo_stage;       // heavy histories -> the memo stage
     const bool coop = spread && !memo0 && c->heavy_stage != 1;
     const bool use_spread = spread && !memo0 && c->heavy_stage != 0;
-    const uint64_t g_heavy = memo0 ? c->memo_grid : (coop ? c->coop_grid : 0) + (use_spread ? kSpreadFinalGrid : 0);
+    // memo grids: outside heavy mode few histories reach the memo stage
+    const uint64_t g_m0 = (c->stage0_auto && !c->auto_heavy) ? std::min<uint64_t>(c->memo_grid, kQuietMemoGrid)
+                                                               : c->memo_grid;
+    const uint64_t g_mw = c->memo_grid;
+    const uint64_t g_heavy = memo0 ? g_m0 : (coop ? c->coop_grid : 0) + (use_spread ? kSpreadFinalGrid : 0);
     const uint64_t g0b = spread ? g_heavy + (memo0 ? 0 : kRedoGrid) : (grp_redo ? kRedoGrid : 0);
     const uint64_t gfx = early ? std::min<uint64_t>(std::max<uint64_t>((n_hist + 63) / 64, 1), 4096) : 0;
     const bool split = c->split_budget && (!max_nodes || c->split_budget < max_nodes);
@@ -461,7 +466,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // stage 0w over its node budget: coop64 (+ an exact redo when no split takes the capped ones)
     const bool heavy_w = gw0 && c->stage0w_budget && (!max_nodes || c->stage0w_budget < max_nodes);
     const bool memo_w = heavy_w && c->memo_stage;
-    const uint64_t gwh = memo_w ? c->memo_grid : heavy_w ? c->coop64_grid + (split ? 0 : kRedoGrid) : 0;
+    const uint64_t gwh = memo_w ? g_mw : heavy_w ? c->coop64_grid + (split ? 0 : kRedoGrid) : 0;
     const uint64_t gw = gw0 + gwh;
     const uint64_t n_part = g0r + g0b + gw + kStage1Grid + kStage2Grid + gsp + gfx;
     // counters: [0] stage-1 list, [1] stage-2 list, [2] timed out, [3] unused,
@@ -516,9 +521,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     unsigned long long* part = reinterpret_cast<unsigned long long*>(c->ws + off_part);
     if (early && !nodes) nodes = reinterpret_cast<uint64_t*>(c->ws + off_nd);
 
-    HIP_TRY(c, hipMemsetAsync(cnt, 0, 128, s), "memset counters");
-    HIP_TRY(c, hipMemsetAsync(cnt + 6, 0xFF, 4, s), "memset first_fail");
-    HIP_TRY(c, hipMemsetAsync(tot, 0, sizeof(qsmd_totals), s), "memset totals");
+    HIP_TRY(c, launch_prep(cnt, tot, s), "prep launch");
     a.first_fail = early ? cnt + 6 : nullptr;
 
     a.hdr = hdr;
@@ -626,7 +629,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         mp.entries = (uint32_t)c->mt_entries;
         mp.epoch = c->mt_epoch;
         mp.stats = c->memo_stats;
-        HIP_TRY(c, launch_memo(mp, (uint32_t)c->memo_grid, false, s), "memo launch");
+        HIP_TRY(c, launch_memo(mp, (uint32_t)g_m0, false, s), "memo launch");
         c->last_sp_hist = nullptr;
     }
     if (coop) {
@@ -713,7 +716,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp.entries = (uint32_t)c->mt_entries;
             mp.epoch = c->mt_epoch;
             mp.stats = c->memo_stats;
-            HIP_TRY(c, launch_memo(mp, (uint32_t)c->memo_grid, true, s), "memo64 launch");
+            HIP_TRY(c, launch_memo(mp, (uint32_t)g_mw, true, s), "memo64 launch");
         } else if (heavy_w) {
             // one wavefront per heavy history; one that explores more than the
             // cap goes to the split stage (giants), or to an exact per-lane redo

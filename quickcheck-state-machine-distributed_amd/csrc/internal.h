@@ -228,6 +228,7 @@ struct CoopArgs {
 
 hipError_t launch_coop(const CoopArgs& p, uint32_t grid, hipStream_t s);
 hipError_t launch_coop64(const CoopArgs& p, uint32_t grid, hipStream_t s);
+hipError_t launch_prep(uint32_t* cnt, qsmd_totals* totals, hipStream_t s);
 
 // memo stage (csrc/memo.hip): per-lane search of a compact stage's heavy
 // histories (s.list / s.list_count) with an exact-count state memo; one

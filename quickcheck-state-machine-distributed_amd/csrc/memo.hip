@@ -127,7 +127,7 @@ __device__ __forceinline__ void memo_insert(uint32_t* tab, const MemoKey<MODEL, 
 template <uint32_t MODEL, class G, int MODE>
 __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* evc,
                                          int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* tab,
-                                         uint32_t h, uint32_t epoch, uint32_t mask, uint64_t* entry, bool& skip,
+                                         uint32_t h, uint32_t epoch, uint32_t mask, uint32_t* entry, bool& skip,
                                          MemoStats& ms) {
     using M = typename G::M;
     const bool empty = d.cand == (M)0;
@@ -136,11 +136,12 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
                        : ((!d.found && d.depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE);
     if (empty & !term) {
         // leaving the node at depth d.depth: its subtree was searched to the end and failed
-        if (!skip) {
-            const uint64_t cnt = d.nodes - entry[(d.depth - 1u) * C_LANES];
+        // (counts kept mod 2^32: exact while the running count is below 2^32)
+        if (!skip && d.nodes <= 0xFFFFFFFFull) {
+            const uint32_t cnt = (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES];
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
-            if (k.ok && cnt <= 0xFFFFFFFFull) {
-                memo_insert<MODEL, G>(tab, k, h, (uint32_t)cnt);
+            if (k.ok) {
+                memo_insert<MODEL, G>(tab, k, h, cnt);
                 ++ms.inserts;
             }
         }
@@ -153,7 +154,7 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
         const uint32_t dep0 = d.depth;
         status = d.template try_next<C_LANES, MODE>(a, evc, s_bal, lane, limit);
         if (d.depth > dep0) {                     // entered a new node
-            entry[dep0 * C_LANES] = d.nodes;
+            entry[dep0 * C_LANES] = (uint32_t)d.nodes;
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             uint32_t cnt = 0;
             if (k.ok && memo_lookup<MODEL, G>(tab, k, h, cnt)) {
@@ -178,13 +179,13 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
 // list mode over a.list (the heavy histories of a compact stage); every
 // history of the list fits geometry G (it was staged there before)
 template <uint32_t MODEL, class G>
-__global__ __launch_bounds__(C_LANES, 2) void memo_search(MemoArgs p) {
+__global__ __launch_bounds__(C_LANES, G::EV == 32 ? 3 : 2) void memo_search(MemoArgs p) {
     constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
     using M = typename G::M;
     const SearchArgs& a = p.s;
     __shared__ uint32_t s_ev[G::EV][C_LANES];
     __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
-    __shared__ uint64_t s_entry[G::LEVELS][C_LANES];
+    __shared__ uint32_t s_entry[G::LEVELS][C_LANES];
 
     const int lane = threadIdx.x;
     const uint64_t total = *a.list_count;

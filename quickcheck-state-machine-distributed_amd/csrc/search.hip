@@ -364,6 +364,20 @@ __global__ __launch_bounds__(256) void reduce_totals_kernel(const unsigned long 
     }
 }
 
+// One launch instead of three memsets before a call: the 32 stage counters
+// (counter 6 = first failing history = none), and the totals the reduce
+// kernel accumulates into.
+__global__ __launch_bounds__(64) void prep_kernel(uint32_t* cnt, unsigned long long* totals) {
+    const uint32_t t = threadIdx.x;
+    if (t < 32u) cnt[t] = t == 6u ? 0xFFFFFFFFu : 0u;
+    if (t < (uint32_t)T_N) totals[t] = 0ull;
+}
+
+hipError_t launch_prep(uint32_t* cnt, qsmd_totals* totals, hipStream_t s) {
+    hipLaunchKernelGGL(prep_kernel, dim3(1), dim3(64), 0, s, cnt, reinterpret_cast<unsigned long long*>(totals));
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ launch
 
 namespace {
