@@ -71,6 +71,8 @@ struct qsmd_ctx {
     size_t mt_bytes = 0;
     uint32_t mt_epoch = 0;
     unsigned long long* memo_stats = nullptr;   // diagnostic (memo_stats_ptr)
+    uint64_t cut_k = 0;                // straggler cut: lanes still searching when a wave cuts them (0 = off)
+    uint64_t cut_min = 16;             // ... after this many iterations
     uint64_t rerun_budget = 0;         // stage 0 budget before the lane re-run (stage 0r); 0 = none
     uint64_t stage0w = 1;              // 33..64-event histories in the compact kernel (else stage 1)
     uint64_t stage0w_budget = 32;      // stage 0w: nodes per history before the memo stage (coop64 without it; 0 = none)
@@ -212,7 +214,7 @@ int qsmd_open(qsmd_ctx** out, int device) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
     if (hipEventCreateWithFlags(&c->probe_ev, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&c->probe_host), 8, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(reinterpret_cast<void**>(&c->probe_host), 16, hipHostMallocDefault) != hipSuccess) {
         qsmd_close(c);
         return QSMD_ERR_DEVICE;
     }
@@ -303,6 +305,11 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->memo_grid = value;
     } else if (n == "memo_stats_ptr") {     // diagnostic: device buffer of 3 x u64 (iterations, hits, inserts)
         c->memo_stats = reinterpret_cast<unsigned long long*>(value);
+    } else if (n == "cut_k") {
+        if (value > 63) return fail(c, QSMD_ERR_ARG, "cut_k in 0..63");
+        c->cut_k = value;
+    } else if (n == "cut_min") {
+        c->cut_min = std::min<uint64_t>(value, 0xFFFFFFFFull);
     } else if (n == "rerun_budget") {
         c->rerun_budget = value;
     } else if (n == "stage0w") {
@@ -430,7 +437,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // re-search, kRedoGrid); group_search shares them in-wave instead
     // adaptive cascade: the decision of the last probe that has landed
     if (c->stage0_auto && c->probe_pending && hipEventQuery(c->probe_ev) == hipSuccess) {
-        const uint64_t longs = (uint64_t)c->probe_host[0] + c->probe_host[1];
+        // heavy-list entries (minus the cut stragglers) + long finished searches
+        const uint64_t longs = (uint64_t)c->probe_host[0] - std::min(c->probe_host[0], c->probe_host[2]) +
+                               c->probe_host[1];
         c->auto_heavy = longs * kAutoFrac >= std::max<uint64_t>(c->probe_n_hist, 1);
         c->probe_pending = false;
     }
@@ -562,6 +571,11 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         a0.heavy_list = lh;
         a0.heavy_count = cnt + 4;
         a0.stage0_budget = budget0;
+        if (memo0 && c->cut_k) {        // stragglers -> the memo stage as well
+            a0.cut_k = (uint32_t)c->cut_k;
+            a0.cut_min = (uint32_t)c->cut_min;
+            a0.cut_count = cnt + 28;
+        }
     } else if (split) {                 // stage 0 -> split
         a0.heavy_list = lg;
         a0.heavy_count = cnt + 7;
@@ -699,6 +713,10 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             aw.heavy_list = lwh;
             aw.heavy_count = cnt + 24;
             aw.stage0_budget = c->stage0w_budget;
+            if (memo_w && c->cut_k) {   // stragglers -> the memo stage as well
+                aw.cut_k = (uint32_t)c->cut_k;
+                aw.cut_min = (uint32_t)c->cut_min;
+            }
         } else if (split) {             // as stage 0 without a budget: -> split
             aw.heavy_list = lg;
             aw.heavy_count = cnt + 7;
@@ -810,6 +828,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     if (probe) {                        // heavy mode: the heavy list is the probe
         // long searches: finished ones over kAutoProbe nodes + the ones over the budget
         HIP_TRY(c, hipMemcpyAsync(c->probe_host + 1, cnt + 22, 4, hipMemcpyDeviceToHost, s), "probe read-back");
+        HIP_TRY(c, hipMemcpyAsync(c->probe_host + 2, cnt + 28, 4, hipMemcpyDeviceToHost, s), "probe read-back");
         HIP_TRY(c, hipMemcpyAsync(c->probe_host, spread ? cnt + 4 : cnt + 3, 4, hipMemcpyDeviceToHost, s),
                 "probe read-back");
         HIP_TRY(c, hipEventRecord(c->probe_ev, s), "hipEventRecord");

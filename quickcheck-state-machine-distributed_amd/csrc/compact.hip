@@ -52,7 +52,12 @@ __device__ __forceinline__ int run_search(DFS& dfs, const SearchArgs& a, const u
     uint32_t iter = 0;
     do {                                 // one exit (see LaneDFS::step)
         status = dfs.template step<C_LANES, MODE>(a, evc, s_bal, lane, limit);
-        if (((++iter) & 1023u) == 0u && status < 0) {
+        ++iter;
+        if (a.cut_k && (iter & 3u) == 0u && iter >= a.cut_min) {   // straggler cut (wave-uniform test)
+            const uint64_t live = __ballot(status < 0);
+            if ((uint32_t)__builtin_popcountll(live) <= a.cut_k && status < 0) status = QSMD_STATUS_HANDED_OFF;
+        }
+        if ((iter & 1023u) == 0u && status < 0) {
             if (beyond_first_fail(a, h)) {
                 status = QSMD_STATUS_SKIPPED;
             } else if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
@@ -161,8 +166,14 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
             st_acc[1] += ts_a - ts_b;
         }
         // over the stage-0 budget (not the caller's): restart in the refill stage
-        const bool heavy = tiered && status == QSMD_STATUS_BUDGET && dfs.nodes >= limit;
+        // (or cut as a straggler)
+        const bool cut = status == QSMD_STATUS_HANDED_OFF;
+        const bool heavy = (tiered && status == QSMD_STATUS_BUDGET && dfs.nodes >= limit) || cut;
         wave_append(heavy, h, a.heavy_list, a.heavy_count, lane);
+        if (a.cut_count) {
+            const uint64_t cm = __ballot(cut);
+            if (cm && lane == __builtin_ctzll(cm)) atomicAdd(a.cut_count, (uint32_t)__builtin_popcountll(cm));
+        }
         if (heavy) {
             base = base_next;
             continue;

@@ -61,7 +61,17 @@ struct SearchArgs {
     // probe_nodes nodes (null = no probe)
     uint32_t* probe;
     uint64_t probe_nodes;
+    // straggler cut (compact stages with a heavy list): once a wavefront has
+    // run cut_min iterations and at most cut_k of its lanes still search,
+    // those lanes stop and their histories go to the heavy list (searched
+    // again from the root there); cut_count counts them.  0 = off.
+    uint32_t cut_k;
+    uint32_t cut_min;
+    uint32_t* cut_count;
 };
+
+// internal status: the search was handed to a later stage (not a result)
+constexpr int QSMD_STATUS_HANDED_OFF = 0x40;
 
 // The per-lane node limit of a stage, and whether reaching it hands the
 // history to the split stage (rather than being the caller's BUDGET).

@@ -50,8 +50,6 @@ struct MemoKey {
     bool ok;
 };
 
-constexpr int QSMD_STATUS_HANDED_OFF = 0x40;   // internal: past the giant cap
-
 struct MemoStats {
     uint64_t iters, hits, inserts;
 };

@@ -210,6 +210,25 @@ def test_memo_stage(ctx, name, n, budget, max_nodes, entries):
         ctx.set_param("stage0_auto", 1)
 
 
+@pytest.mark.parametrize("name,n", [("bank_4x16", 50000), ("bank_4x16_bugs", 30000), ("ticket_2x10", 20000),
+                                    ("bank_6x24", 20000)])
+@pytest.mark.parametrize("cut_k,cut_min", [(2, 16), (8, 4), (63, 4)])
+def test_straggler_cut(ctx, name, n, cut_k, cut_min):
+    """Straggler cut: once a wavefront has run cut_min iterations with at most
+    cut_k lanes still searching, those histories go to the memo stage and are
+    searched again from the root (63: nearly every history is cut)."""
+    ctx.set_param("cut_k", cut_k)
+    ctx.set_param("cut_min", cut_min)
+    try:
+        hdr, ev, _ = gen.generate_config(name, 13, n)
+        for _ in range(2):                       # the cascade's quiet mode, then its decision
+            _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=30)
+    finally:
+        ctx.set_param("cut_k", 0)
+        ctx.set_param("cut_min", 16)
+
+
 @pytest.mark.parametrize("split_budget", [16, 200])
 def test_memo_stage_handoff(ctx, split_budget):
     """Memo-stage searches that reach the giant cap (= split budget
