@@ -31,7 +31,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402  (first: our library shares torch's HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
-from qsmd import device, gen  # noqa: E402
+from qsmd import codec, device, gen  # noqa: E402
 
 METRIC = ("histories checked/sec (whole node) + search nodes/sec, "
           "4×16-op Bank, 1/2/4/8 GPU")
@@ -69,10 +69,18 @@ def cpu_baseline(hdr, ev, model_id, target_s):
         nodes += float(nd.astype(np.float64).sum())
         passes += 1
     n = len(hdr) * passes
+    # SURVEY.md §8d also asks for the same port on every host core (history shards per thread)
+    threads = min(16, os.cpu_count() or 1)
+    t = time.perf_counter()
+    oracle_c.check_batch(model_id, hdr, ev, threads=threads)
+    dt_mt = time.perf_counter() - t
     return {"value": n / dt, "unit": "histories/s", "cores": 1, "kind": "port",
             "sample": f"{passes} pass(es) over the {len(hdr)} rank-0 histories, 1 thread, {dt:.1f} s, "
                       f"oracle/ref_cpu.c -O3 (reference semantics, no memo)",
-            "nodes_per_sec": nodes / dt}, st, nd, len(hdr)
+            "nodes_per_sec": nodes / dt,
+            "multi_thread": {"value": len(hdr) / dt_mt, "cores": threads,
+                             "sample": f"1 pass over the {len(hdr)} histories, {threads} threads, {dt_mt:.2f} s"}}, \
+        st, nd, len(hdr)
 
 
 def main():
@@ -88,6 +96,8 @@ def main():
                     help="per-lane node budget before the split stage (library default if unset)")
     ap.add_argument("--stage0-budget", type=int, default=None)
     ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")
+    ap.add_argument("--device-gen", action="store_true",
+                    help="generate the batch on the GPU (qsmd_gen_batch_device; same histories as the host generator)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC summary written by profiles/profile.sh (for roofline.traffic)")
     args = ap.parse_args()
@@ -103,18 +113,29 @@ def main():
     cfg = dict(gen.CONFIGS[args.config])
     model_id = cfg["model_id"]
     n = args.n_hist
-    t = time.perf_counter()
-    hdr, ev, bug = gen.generate(gen.params(**cfg), rank * n, n, threads=min(16, os.cpu_count() or 1))
-    log(f"[rank {rank}] generated {n} histories in {time.perf_counter() - t:.1f}s")
-
     ctx = device.Context(local)
+    t = time.perf_counter()
+    if args.device_gen:                   # on-device generation (csrc/gen.hip), same stream as the host's
+        per = 2 * cfg["n_ops"]
+        d_hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+        d_ev = torch.empty(n * per * 8, dtype=torch.uint8, device=dev)
+        ctx.gen_device(gen.params(**cfg), rank * n, n, d_hdr.data_ptr(), d_ev.data_ptr(),
+                       stream=torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        hdr = d_hdr.cpu().numpy().view(codec.HDR_DTYPE)
+        ev = d_ev.cpu().numpy().view(codec.EV_DTYPE)
+    else:
+        hdr, ev, bug = gen.generate(gen.params(**cfg), rank * n, n, threads=min(16, os.cpu_count() or 1))
+        d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
+        d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
+    log(f"[rank {rank}] generated {n} histories ({'device' if args.device_gen else 'host'}) "
+        f"in {time.perf_counter() - t:.2f}s")
+
     if args.split_budget is not None:
         ctx.set_split_budget(args.split_budget)
     if args.stage0_budget is not None:
         ctx.set_stage0_budget(args.stage0_budget)
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
-    d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
-    d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
     d_st = torch.empty(n, dtype=torch.uint8, device=dev)
     d_nd = torch.empty(n, dtype=torch.int64, device=dev)
     d_tot = torch.zeros(8, dtype=torch.int64, device=dev)
@@ -171,7 +192,8 @@ def main():
         "metric": METRIC, "value": value, "unit": "histories/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
-        "data": "synthetic (seeded scheduler-policy generator, include/qsmd_gen.h)",
+        "data": "synthetic (seeded scheduler-policy generator, include/qsmd_gen.h" +
+                (", generated on the GPU)" if args.device_gen else ")"),
         "config": {"workload": args.config, "histories_per_gpu": n,
                    "clients": cfg["n_clients"], "ops": cfg["n_ops"],
                    "events_per_history": 2 * cfg["n_ops"], "parallelism": f"shard{world}",

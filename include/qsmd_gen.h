@@ -57,6 +57,14 @@ int qsmd_gen_batch(const qsmd_gen_params* p, uint64_t first, uint64_t n_hist,
                    uint32_t ev_base, qsmd_hdr* hdr, qsmd_event* events,
                    uint8_t* bug_out, int n_threads);
 
+/* On-device generation (libqsmd.so, csrc/gen.hip): the same stream as
+ * qsmd_gen_batch, byte-identical, written to device buffers (hdr_dev[n_hist],
+ * events_dev[n_hist * 2 * n_ops], bug_dev nullable) and enqueued on `stream`
+ * (NULL = the context's stream) of ctx's device.  Returns 0 or QSMD_ERR_*. */
+int qsmd_gen_batch_device(qsmd_ctx* ctx, const qsmd_gen_params* p, uint64_t first, uint64_t n_hist,
+                          uint32_t ev_base, qsmd_hdr* hdr_dev, qsmd_event* events_dev,
+                          uint8_t* bug_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

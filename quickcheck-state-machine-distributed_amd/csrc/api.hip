@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "internal.h"
+#include "qsmd_gen.h"
 #include "qsmd.h"
 
 using namespace qsmd;
@@ -918,6 +919,24 @@ static int wellformed_locked(qsmd_ctx* c, const qsmd_hdr* hdr, uint64_t n_hist, 
     HIP_TRY(c, launch_wellformed(hdr, n_hist, reinterpret_cast<const uint2*>(events), n_events,
                                  reinterpret_cast<const uint8_t*>(c->wf_rank_dev), out, grid, s),
             "wellformed launch");
+    return QSMD_OK;
+}
+
+int qsmd_gen_batch_device(qsmd_ctx* c, const qsmd_gen_params* p, uint64_t first, uint64_t n_hist, uint32_t ev_base,
+                          qsmd_hdr* hdr_dev, qsmd_event* events_dev, uint8_t* bug_dev, void* stream) {
+    if (!c) return QSMD_ERR_ARG;
+    // the parameter checks of qsmd_gen_batch (csrc/gen/gen.cpp)
+    if (!p || (n_hist && (!hdr_dev || !events_dev))) return fail(c, QSMD_ERR_ARG, "null params/buffers");
+    if (p->model_id != QSMD_MODEL_BANK && p->model_id != QSMD_MODEL_TICKET) return fail(c, QSMD_ERR_ARG, "model_id");
+    if (p->n_clients < 1 || p->n_clients > QSMD_BANK_MAX_ACCOUNTS) return fail(c, QSMD_ERR_ARG, "n_clients");
+    if (p->n_ops < 1 || 2 * p->n_ops > QSMD_MAX_EVENTS) return fail(c, QSMD_ERR_ARG, "n_ops");
+    if (p->model_id == QSMD_MODEL_BANK && p->n_ops < p->n_clients) return fail(c, QSMD_ERR_ARG, "n_ops < n_clients");
+    if ((uint64_t)ev_base + n_hist * 2ull * p->n_ops > 0xFFFFFFFFull) return fail(c, QSMD_ERR_ARG, "ev_off beyond u32");
+    if (n_hist == 0) return QSMD_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
+    HIP_TRY(c, launch_gen(*p, first, n_hist, ev_base, hdr_dev, events_dev, bug_dev,
+                          stream ? static_cast<hipStream_t>(stream) : c->stream), "gen launch");
     return QSMD_OK;
 }
 

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "qsmd.h"
+#include "qsmd_gen.h"
 
 namespace qsmd {
 
@@ -239,6 +240,8 @@ struct CoopArgs {
 hipError_t launch_coop(const CoopArgs& p, uint32_t grid, hipStream_t s);
 hipError_t launch_coop64(const CoopArgs& p, uint32_t grid, hipStream_t s);
 hipError_t launch_prep(uint32_t* cnt, qsmd_totals* totals, hipStream_t s);
+hipError_t launch_gen(const qsmd_gen_params& p, uint64_t first, uint64_t n_hist, uint32_t ev_base, qsmd_hdr* hdr,
+                      qsmd_event* events, uint8_t* bug_out, hipStream_t s);
 
 // memo stage (csrc/memo.hip): per-lane search of a compact stage's heavy
 // histories (s.list / s.list_count) with an exact-count state memo; one

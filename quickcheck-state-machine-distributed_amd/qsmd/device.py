@@ -66,6 +66,7 @@ EXPORTS = {
     "qsmd_spread_stats": (_I, [_P, _P]),
     "qsmd_wellformed_batch": (_I, [_P, _P, _U64, _P, _U64, _P, _U32, _P]),
     "qsmd_wellformed_batch_device": (_I, [_P, _P, _U64, _P, _U64, _P, _U32, _P, _P]),
+    "qsmd_gen_batch_device": (_I, [_P, _P, _U64, _U64, _U32, _P, _P, _P, _P]),   # include/qsmd_gen.h
     "qsmd_check_batch": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P]),
     "qsmd_check_batch_device": (_I, [_P, _U32, _P, _U64, _P, _U64, _P, _U32, _U64, _P, _P, _P, _P, _P]),
     "qsmd_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
@@ -283,6 +284,14 @@ class Context:
             self._h, hdr_ptr, n_hist, events_ptr, n_events, _ptr(pl) if pl is not None and len(pl) else None,
             0 if pl is None else len(pl), out_ptr, stream)
         self._check(rc, "qsmd_wellformed_batch_device")
+
+    def gen_device(self, params, first, n_hist, hdr_ptr, events_ptr, bug_ptr=None, ev_base=0, stream=None):
+        """On-device synthetic generation (include/qsmd_gen.h
+        qsmd_gen_batch_device): the qsmd.gen stream [first, first + n_hist),
+        byte-identical to the host generator, into device buffers (async)."""
+        rc = self._lib.qsmd_gen_batch_device(self._h, ctypes.byref(params), first, n_hist, ev_base, hdr_ptr,
+                                             events_ptr, bug_ptr, stream)
+        self._check(rc, "qsmd_gen_batch_device")
 
     def spread_stats(self):
         """Spread stage of the last call: (histories, tasks, explored nodes,
