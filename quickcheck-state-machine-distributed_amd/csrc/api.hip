@@ -447,6 +447,19 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // (with the memo stage, a call that is not in heavy mode still sends the
     // histories over the split budget to it: it searches most of them in far
     // fewer nodes, and hands the rest to the split stage)
+    // memo tables first: if the device cannot hold them, this context runs
+    // without the memo stage (coop / spread take the heavy histories: the
+    // same results, more work)
+    const uint64_t mt_slots = c->memo_grid * C_LANES_HOST * c->mt_entries;
+    if (c->memo_stage && c->mt_bytes < (size_t)mt_slots * (32 + 64)) {
+        if (grow(c, &c->mt, &c->mt_bytes, (size_t)mt_slots * (32 + 64)) != QSMD_OK) {
+            (void)hipGetLastError();     // clear the allocation error: later launches check it
+            c->memo_stage = 0;
+            c->err = "memo tables do not fit on the device: memo stage off for this context";
+        } else {
+            HIP_TRY(c, hipMemsetAsync(c->mt, 0, c->mt_bytes, s), "memset memo tables");
+        }
+    }
     const uint64_t quiet0 = c->memo_stage ? std::min<uint64_t>(c->split_budget, kQuietBudget) : 0;
     const uint64_t budget0 = c->stage0_auto ? (c->auto_heavy ? kAutoBudget : quiet0) : c->stage0_budget;
     const bool probe = c->stage0_auto && !grp && !persistent && !c->probe_pending;
@@ -512,14 +525,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         if (rc) return rc;
         HIP_TRY(c, hipMemsetAsync(c->spt, 0, c->spt_bytes, s), "memset spread tasks");
     }
-    const uint64_t mt_slots = c->memo_grid * C_LANES_HOST * c->mt_entries;
-    const size_t mt_need = (memo0 || memo_w) ? (size_t)mt_slots * (32 + 64) : 0;
-    if (mt_need && c->mt_bytes < mt_need) {
-        rc = grow(c, &c->mt, &c->mt_bytes, mt_need);
-        if (rc) return rc;
-        HIP_TRY(c, hipMemsetAsync(c->mt, 0, c->mt_bytes, s), "memset memo tables");
-    }
-    if (mt_need && ((++c->mt_epoch) & 0xFFFFFFu) == 0u) {   // 24-bit tags wrapped: clear
+    const bool mt_used = memo0 || memo_w;
+    if (mt_used && ((++c->mt_epoch) & 0xFFFFFFu) == 0u) {   // 24-bit tags wrapped: clear
         HIP_TRY(c, hipMemsetAsync(c->mt, 0, c->mt_bytes, s), "memset memo tables");
         ++c->mt_epoch;
     }

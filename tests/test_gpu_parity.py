@@ -229,6 +229,21 @@ def test_straggler_cut(ctx, name, n, cut_k, cut_min):
         ctx.set_param("cut_min", 16)
 
 
+def test_memo_tables_too_large_fall_back_to_coop_spread(ctx):
+    """Memo tables the device cannot hold switch the context to the coop /
+    spread heavy stages: the same results."""
+    ctx.set_param("memo_grid", 65536)
+    ctx.set_param("memo_lane_entries", 65536)
+    try:
+        hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 21, 20000)
+        for _ in range(2):
+            _compare(ctx, models.MODEL_BANK, hdr, ev)
+    finally:
+        ctx.set_param("memo_grid", 2048)
+        ctx.set_param("memo_lane_entries", 256)
+        ctx.set_param("memo_stage", 1)
+
+
 @pytest.mark.parametrize("split_budget", [16, 200])
 def test_memo_stage_handoff(ctx, split_budget):
     """Memo-stage searches that reach the giant cap (= split budget
