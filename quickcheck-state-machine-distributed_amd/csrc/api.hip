@@ -67,6 +67,7 @@ struct qsmd_ctx {
     uint64_t stage0_dynamic = 0;       // compact_search: groups from a counter (persistent grid)
     uint64_t memo_stage = 1;           // heavy histories: the memo stage (exact-count state memo, csrc/memo.hip)
     uint64_t mt_entries = 256;         // memo stage: table entries per lane (power of two)
+    uint64_t memo_min_rem = 0;         // memo stage: states with at most this many events left are not memoised
     uint64_t memo_grid = 2048;         // memo stage: workgroups (table slots = memo_grid * 64)
     char* mt = nullptr;                // memo stage tables: [G32 region][G64 region]
     size_t mt_bytes = 0;
@@ -301,6 +302,8 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         if (value < 2 || value > 65536 || (value & (value - 1)))
             return fail(c, QSMD_ERR_ARG, "memo_lane_entries: a power of two in 2..65536");
         c->mt_entries = value;
+    } else if (n == "memo_min_rem") {
+        c->memo_min_rem = std::min<uint64_t>(value, 128);
     } else if (n == "memo_grid") {
         if (value < 1 || value > 65536) return fail(c, QSMD_ERR_ARG, "memo_grid in 1..65536");
         c->memo_grid = value;
@@ -649,6 +652,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         }
         mp.table = reinterpret_cast<uint32_t*>(c->mt);
         mp.entries = (uint32_t)c->mt_entries;
+        mp.min_rem = (uint32_t)c->memo_min_rem;
         mp.epoch = c->mt_epoch;
         mp.stats = c->memo_stats;
         HIP_TRY(c, launch_memo(mp, (uint32_t)g_m0, false, s), "memo launch");
@@ -740,6 +744,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp.s.partials = part + (g0r + g0b + gw0) * T_N;
             mp.table = reinterpret_cast<uint32_t*>(c->mt + (size_t)mt_slots * 32);
             mp.entries = (uint32_t)c->mt_entries;
+            mp.min_rem = (uint32_t)c->memo_min_rem;
             mp.epoch = c->mt_epoch;
             mp.stats = c->memo_stats;
             HIP_TRY(c, launch_memo(mp, (uint32_t)g_mw, true, s), "memo64 launch");

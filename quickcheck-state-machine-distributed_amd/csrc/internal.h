@@ -251,8 +251,9 @@ struct MemoArgs {
     uint32_t* table;              // grid * 64 * entries * (8 | 16) u32
     uint32_t entries;
     uint32_t epoch;               // this call's tag (24 bits)
-    unsigned long long* stats;    // diagnostic: iterations, hits, inserts (null = off)
+    unsigned long long* stats;    // diagnostic: iterations, hits, inserts, max per history (null = off)
     uint64_t giant_cap;           // > 0: a search past this many iterations goes to s.giant_list
+    uint32_t min_rem;             // states with at most this many events left are not memoised
 };
 hipError_t launch_memo(const MemoArgs& p, uint32_t grid, bool wide, hipStream_t s);
 

@@ -51,7 +51,7 @@ struct MemoKey {
 };
 
 struct MemoStats {
-    uint64_t iters, hits, inserts;
+    uint64_t iters, hits, inserts, max_iters;
 };
 
 __device__ __forceinline__ uint32_t mix32(uint32_t h) {
@@ -126,7 +126,7 @@ template <uint32_t MODEL, class G, int MODE>
 __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* evc,
                                          int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* tab,
                                          uint32_t h, uint32_t epoch, uint32_t mask, uint32_t* entry, bool& skip,
-                                         MemoStats& ms) {
+                                         uint32_t min_rem, MemoStats& ms) {
     using M = typename G::M;
     const bool empty = d.cand == (M)0;
     const bool term = empty & ((d.found == 0u) | (d.depth == d.base));
@@ -135,7 +135,8 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     if (empty & !term) {
         // leaving the node at depth d.depth: its subtree was searched to the end and failed
         // (counts kept mod 2^32: exact while the running count is below 2^32)
-        if (!skip && d.nodes <= 0xFFFFFFFFull) {
+        // (small subtrees -- at most min_rem events left -- are cheaper to search than to look up)
+        if (!skip && d.nodes <= 0xFFFFFFFFull && (uint32_t)__builtin_popcountll((uint64_t)d.rem) > min_rem) {
             const uint32_t cnt = (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES];
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             if (k.ok) {
@@ -153,9 +154,10 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
         status = d.template try_next<C_LANES, MODE>(a, evc, s_bal, lane, limit);
         if (d.depth > dep0) {                     // entered a new node
             entry[dep0 * C_LANES] = (uint32_t)d.nodes;
+            const bool big = (uint32_t)__builtin_popcountll((uint64_t)d.rem) > min_rem;
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             uint32_t cnt = 0;
-            if (k.ok && memo_lookup<MODEL, G>(tab, k, h, cnt)) {
+            if (big && k.ok && memo_lookup<MODEL, G>(tab, k, h, cnt)) {
                 ++ms.hits;
                 if (d.nodes + cnt > limit) {      // the budget falls inside that subtree
                     d.nodes = limit;
@@ -188,7 +190,7 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 3 : 2) void memo_search(Memo
     const int lane = threadIdx.x;
     const uint64_t total = *a.list_count;
     Counters cnt;
-    MemoStats ms{0, 0, 0};
+    MemoStats ms{0, 0, 0, 0};
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
     uint32_t* tab = p.table + ((uint64_t)blockIdx.x * C_LANES + (uint64_t)lane) * (uint64_t)p.entries *
@@ -227,7 +229,7 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 3 : 2) void memo_search(Memo
             uint32_t iter = 0;
             do {
                 status = memo_step<MODEL, G, M_LANE>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, tab, h, p.epoch,
-                                                     mask, &s_entry[0][lane], skip, ms);
+                                                     mask, &s_entry[0][lane], skip, p.min_rem, ms);
                 ++iter;
                 if (p.giant_cap && iter >= p.giant_cap && status < 0) {
                     status = QSMD_STATUS_HANDED_OFF;
@@ -241,6 +243,7 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 3 : 2) void memo_search(Memo
                 }
             } while (status < 0);
             ms.iters += iter;
+            ms.max_iters = ms.max_iters > iter ? ms.max_iters : iter;
         }
         if (status == QSMD_STATUS_HANDED_OFF) {  // the split stage searches it (exact, from the root)
             a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
@@ -260,6 +263,7 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 3 : 2) void memo_search(Memo
             atomicAdd(p.stats + 1, (unsigned long long)hi);
             atomicAdd(p.stats + 2, (unsigned long long)in);
         }
+        atomicMax(p.stats + 3, (unsigned long long)ms.max_iters);
     }
 }
 
