@@ -107,7 +107,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # the counter all-reduce (QSMD_BENCH_DIST=1 exercises it on one rank too)
+    use_dist = world > 1 or os.environ.get("QSMD_BENCH_DIST") == "1"
+    if use_dist:
         dist.init_process_group("nccl", device_id=dev)
 
     cfg = dict(gen.CONFIGS[args.config])
@@ -138,31 +140,47 @@ def main():
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
     d_st = torch.empty(n, dtype=torch.uint8, device=dev)
     d_nd = torch.empty(n, dtype=torch.int64, device=dev)
-    d_tot = torch.zeros(8, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
+    # Totals ring: step k's counters are all-reduced (RCCL) on a side stream
+    # while step k+1 searches; a slot is reused only after its all-reduce.
+    ring = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(4)]
+    reduced = [None] * len(ring)
+    side = torch.cuda.Stream(dev) if use_dist and os.environ.get("QSMD_BENCH_AR", "inline") == "side" else None
+    k_step = [0]
 
     def step():
+        i = k_step[0] % len(ring)
+        k_step[0] += 1
+        if reduced[i] is not None:
+            stream.wait_event(reduced[i])
         ctx.check_device(model_id, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st.data_ptr(),
-                         d_nd.data_ptr(), None, d_tot.data_ptr(), flags=flags, stream=stream.cuda_stream)
-        if world > 1:
-            dist.all_reduce(d_tot, op=dist.ReduceOp.SUM)
+                         d_nd.data_ptr(), None, ring[i].data_ptr(), flags=flags, stream=stream.cuda_stream)
+        if side is not None:
+            side.wait_stream(stream)
+            with torch.cuda.stream(side):
+                dist.all_reduce(ring[i], op=dist.ReduceOp.SUM)
+                reduced[i] = torch.cuda.Event()
+                reduced[i].record(side)
+        elif use_dist:                    # default: on the search stream (QSMD_BENCH_AR=side: overlapped)
+            dist.all_reduce(ring[i], op=dist.ReduceOp.SUM)
+        return ring[i]
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     ctx.timing_reset()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        d_tot = step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if use_dist:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -217,7 +235,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
