@@ -49,7 +49,8 @@ struct qsmd_ctx {
     bool auto_heavy = false;
     bool probe_pending = false;
     uint64_t probe_n_hist = 0;
-    uint32_t* probe_host = nullptr;    // pinned
+    uint32_t* probe_host = nullptr;    // pinned copy of the 32 stage counters of the probing call
+    bool probe_spread = false;         // that call had a heavy list
     hipEvent_t probe_ev = nullptr;
     uint8_t* wf_rank_host = nullptr;   // wellformed: pid rank table (pinned) and its device copy
     char* wf_rank_dev = nullptr;
@@ -216,7 +217,7 @@ int qsmd_open(qsmd_ctx** out, int device) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->n_cu = prop.multiProcessorCount;
     if (hipEventCreateWithFlags(&c->probe_ev, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&c->probe_host), 16, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(reinterpret_cast<void**>(&c->probe_host), 128, hipHostMallocDefault) != hipSuccess) {
         qsmd_close(c);
         return QSMD_ERR_DEVICE;
     }
@@ -442,8 +443,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // adaptive cascade: the decision of the last probe that has landed
     if (c->stage0_auto && c->probe_pending && hipEventQuery(c->probe_ev) == hipSuccess) {
         // heavy-list entries (minus the cut stragglers) + long finished searches
-        const uint64_t longs = (uint64_t)c->probe_host[0] - std::min(c->probe_host[0], c->probe_host[2]) +
-                               c->probe_host[1];
+        const uint64_t heavy = c->probe_spread ? c->probe_host[4] : 0u;
+        const uint64_t longs = heavy - std::min<uint64_t>(heavy, c->probe_host[28]) + c->probe_host[22];
         c->auto_heavy = longs * kAutoFrac >= std::max<uint64_t>(c->probe_n_hist, 1);
         c->probe_pending = false;
     }
@@ -840,10 +841,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     HIP_TRY(c, hipEventRecord(evs[2], s), "hipEventRecord");
     if (probe) {                        // heavy mode: the heavy list is the probe
         // long searches: finished ones over kAutoProbe nodes + the ones over the budget
-        HIP_TRY(c, hipMemcpyAsync(c->probe_host + 1, cnt + 22, 4, hipMemcpyDeviceToHost, s), "probe read-back");
-        HIP_TRY(c, hipMemcpyAsync(c->probe_host + 2, cnt + 28, 4, hipMemcpyDeviceToHost, s), "probe read-back");
-        HIP_TRY(c, hipMemcpyAsync(c->probe_host, spread ? cnt + 4 : cnt + 3, 4, hipMemcpyDeviceToHost, s),
-                "probe read-back");
+        // (one copy of the 32 stage counters: [4] heavy list, [22] long finished, [28] cut)
+        HIP_TRY(c, hipMemcpyAsync(c->probe_host, cnt, 128, hipMemcpyDeviceToHost, s), "probe read-back");
+        c->probe_spread = spread;
         HIP_TRY(c, hipEventRecord(c->probe_ev, s), "hipEventRecord");
         c->probe_pending = true;
         c->probe_n_hist = n_hist;
