@@ -96,6 +96,8 @@ def main():
                     help="per-lane node budget before the split stage (library default if unset)")
     ap.add_argument("--stage0-budget", type=int, default=None)
     ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="calls in flight (one context + stream each): the next step's search overlaps the tail of the previous one")
     ap.add_argument("--device-gen", action="store_true",
                     help="generate the batch on the GPU (qsmd_gen_batch_device; same histories as the host generator)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -133,37 +135,34 @@ def main():
     log(f"[rank {rank}] generated {n} histories ({'device' if args.device_gen else 'host'}) "
         f"in {time.perf_counter() - t:.2f}s")
 
-    if args.split_budget is not None:
-        ctx.set_split_budget(args.split_budget)
-    if args.stage0_budget is not None:
-        ctx.set_stage0_budget(args.stage0_budget)
+    # S calls in flight (--inflight): one context, stream and output set per
+    # slot; step k runs on slot k % S, so the next batch's stage 0 fills the
+    # compute units the previous call's tail leaves idle.  Each step is the
+    # full search of the batch; a slot's steps are ordered on its stream.
+    S = max(1, args.inflight)
+    ctxs = [ctx] + [device.Context(local) for _ in range(S - 1)]
+    for c in ctxs:
+        if args.split_budget is not None:
+            c.set_split_budget(args.split_budget)
+        if args.stage0_budget is not None:
+            c.set_stage0_budget(args.stage0_budget)
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
-    d_st = torch.empty(n, dtype=torch.uint8, device=dev)
-    d_nd = torch.empty(n, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    # Totals ring: step k's counters are all-reduced (RCCL) on a side stream
-    # while step k+1 searches; a slot is reused only after its all-reduce.
-    ring = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(4)]
-    reduced = [None] * len(ring)
-    side = torch.cuda.Stream(dev) if use_dist and os.environ.get("QSMD_BENCH_AR", "inline") == "side" else None
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev),
+             torch.zeros(8, dtype=torch.int64, device=dev)) for _ in range(S)]
     k_step = [0]
 
     def step():
-        i = k_step[0] % len(ring)
+        i = k_step[0] % S
         k_step[0] += 1
-        if reduced[i] is not None:
-            stream.wait_event(reduced[i])
-        ctx.check_device(model_id, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st.data_ptr(),
-                         d_nd.data_ptr(), None, ring[i].data_ptr(), flags=flags, stream=stream.cuda_stream)
-        if side is not None:
-            side.wait_stream(stream)
-            with torch.cuda.stream(side):
-                dist.all_reduce(ring[i], op=dist.ReduceOp.SUM)
-                reduced[i] = torch.cuda.Event()
-                reduced[i].record(side)
-        elif use_dist:                    # default: on the search stream (QSMD_BENCH_AR=side: overlapped)
-            dist.all_reduce(ring[i], op=dist.ReduceOp.SUM)
-        return ring[i]
+        d_st_i, d_nd_i, d_tot_i = outs[i]
+        ctxs[i].check_device(model_id, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st_i.data_ptr(),
+                             d_nd_i.data_ptr(), None, d_tot_i.data_ptr(), flags=flags,
+                             stream=streams[i].cuda_stream)
+        if use_dist:                      # the counters of this step, on its stream (RCCL)
+            with torch.cuda.stream(streams[i]):
+                dist.all_reduce(d_tot_i, op=dist.ReduceOp.SUM)
+        return i
 
     for _ in range(args.warmup):
         step()
@@ -174,7 +173,7 @@ def main():
     ctx.timing_reset()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        d_tot = step()
+        last = step()
     torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
@@ -186,6 +185,7 @@ def main():
         elapsed = float(e.item())
 
     s0_ms, call_ms = ctx.timing_read()
+    d_st, d_nd, d_tot = outs[last]
     st = d_st.cpu().numpy()
     nd = d_nd.cpu().numpy()
     tot = d_tot.cpu().numpy()               # global totals of the last step
@@ -214,7 +214,7 @@ def main():
                 (", generated on the GPU)" if args.device_gen else ")"),
         "config": {"workload": args.config, "histories_per_gpu": n,
                    "clients": cfg["n_clients"], "ops": cfg["n_ops"],
-                   "events_per_history": 2 * cfg["n_ops"], "parallelism": f"shard{world}",
+                   "events_per_history": 2 * cfg["n_ops"], "parallelism": f"shard{world}", "calls_in_flight": S,
                    "mode": "memo" if args.memo else "exhaustive"},
         "nodes_per_sec": nodes_total * args.steps / elapsed,
         "verdicts": {"checked": int(tot[0]), "linearisable": int(tot[1]),
@@ -234,7 +234,8 @@ def main():
         out["checked_vs_oracle"] = sample
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if use_dist:
         dist.destroy_process_group()
 
