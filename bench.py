@@ -96,8 +96,9 @@ def main():
                     help="per-lane node budget before the split stage (library default if unset)")
     ap.add_argument("--stage0-budget", type=int, default=None)
     ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")
-    ap.add_argument("--inflight", type=int, default=3,
-                    help="calls in flight (one context + stream each): the next step's search overlaps the tail of the previous one")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="calls in flight (one context + stream each): the next step's search overlaps the tail of "
+                         "the previous one; 0 = 3 on one GPU, 2 with RCCL (its stream takes one of the 4 hardware queues)")
     ap.add_argument("--device-gen", action="store_true",
                     help="generate the batch on the GPU (qsmd_gen_batch_device; same histories as the host generator)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -139,7 +140,7 @@ def main():
     # slot; step k runs on slot k % S, so the next batch's stage 0 fills the
     # compute units the previous call's tail leaves idle.  Each step is the
     # full search of the batch; a slot's steps are ordered on its stream.
-    S = max(1, args.inflight)
+    S = args.inflight if args.inflight > 0 else (2 if use_dist else 3)
     ctxs = [ctx] + [device.Context(local) for _ in range(S - 1)]
     for c in ctxs:
         if args.split_budget is not None:
@@ -148,24 +149,54 @@ def main():
             c.set_stage0_budget(args.stage0_budget)
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
-    outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev),
-             torch.zeros(8, dtype=torch.int64, device=dev)) for _ in range(S)]
+    outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
+            for _ in range(S)]
+    # counters: [round parity][slot][8]; the S steps of a round are all-reduced
+    # together (one bucketed RCCL all-reduce per round, on its own stream,
+    # overlapping the next round; a row is reused two rounds later, after it)
+    tot = torch.zeros(2, S, 8, dtype=torch.int64, device=dev)
+    # (the round's all-reduce runs on the last slot's stream: RCCL adds its own
+    # stream, and more streams than hardware queues serialise each other)
+    comm = streams[S - 1] if use_dist else None
+    do_ar = use_dist and os.environ.get("QSMD_BENCH_NOAR") != "1"   # (diagnostic: group without collectives)
+    done = [None, None]                   # per parity: the round's all-reduce finished
     k_step = [0]
 
     def step():
-        i = k_step[0] % S
+        k = k_step[0]
         k_step[0] += 1
-        d_st_i, d_nd_i, d_tot_i = outs[i]
-        ctxs[i].check_device(model_id, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st_i.data_ptr(),
-                             d_nd_i.data_ptr(), None, d_tot_i.data_ptr(), flags=flags,
-                             stream=streams[i].cuda_stream)
-        if use_dist:                      # the counters of this step, on its stream (RCCL)
-            with torch.cuda.stream(streams[i]):
-                dist.all_reduce(d_tot_i, op=dist.ReduceOp.SUM)
-        return i
+        i, par = k % S, (k // S) % 2
+        d_st_i, d_nd_i = outs[i]
+        with torch.cuda.stream(streams[i]):
+            if done[par] is not None:
+                streams[i].wait_event(done[par])
+            ctxs[i].check_device(model_id, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st_i.data_ptr(),
+                                 d_nd_i.data_ptr(), None, tot[par, i].data_ptr(), flags=flags,
+                                 stream=streams[i].cuda_stream)
+        if do_ar and (i == S - 1):        # the round is enqueued: its counters all-reduced together
+            for st_ in streams[:-1]:
+                comm.wait_stream(st_)
+            with torch.cuda.stream(comm):
+                dist.all_reduce(tot[par], op=dist.ReduceOp.SUM)
+                done[par] = torch.cuda.Event()
+                done[par].record(comm)
+        return i, par
+
+    def drain():
+        if k_step[0] % S:                 # a partial last round: reduce it, start the next one fresh
+            if do_ar:
+                par = ((k_step[0] - 1) // S) % 2
+                for st_ in streams[:-1]:
+                    comm.wait_stream(st_)
+                with torch.cuda.stream(comm):
+                    dist.all_reduce(tot[par], op=dist.ReduceOp.SUM)
+                    done[par] = torch.cuda.Event()
+                    done[par].record(comm)
+            k_step[0] = (k_step[0] + S - 1) // S * S
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
@@ -174,6 +205,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         last = step()
+    drain()
     torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
@@ -185,10 +217,10 @@ def main():
         elapsed = float(e.item())
 
     s0_ms, call_ms = ctx.timing_read()
-    d_st, d_nd, d_tot = outs[last]
+    d_st, d_nd = outs[last[0]]
     st = d_st.cpu().numpy()
     nd = d_nd.cpu().numpy()
-    tot = d_tot.cpu().numpy()               # global totals of the last step
+    tot = tot[last[1], last[0]].cpu().numpy()   # global totals of the last step
     ms_per_step = elapsed / args.steps * 1e3
     total_hist = n * world
     value = total_hist * args.steps / elapsed
