@@ -289,6 +289,39 @@ def test_memo_stage_any_shape(ctx, model):
         ctx.set_param("stage0_auto", 1)
 
 
+def test_concurrent_contexts_on_streams(ctx):
+    """bench.py keeps several calls in flight: one context and stream each,
+    running at the same time on one GPU.  Every call's results must be the
+    oracle's (contexts share no device state)."""
+    torch = pytest.importorskip("torch")
+    from qsmd import device
+    dev = torch.device("cuda:0")
+    batches = [gen.generate_config(name, 31, n) for name, n in
+               (("bank_4x16_bugs", 20000), ("bank_4x16", 40000), ("bank_6x24", 8000))]
+    ctxs = [ctx, device.Context(0), device.Context(0)]
+    streams = [torch.cuda.Stream(dev) for _ in ctxs]
+    try:
+        bufs = []
+        for (hdr, ev, _), c, s in zip(batches, ctxs, streams):
+            n = len(hdr)
+            b = (torch.from_numpy(hdr.view(np.uint8)).to(dev), torch.from_numpy(ev.view(np.uint8)).to(dev),
+                 torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
+            bufs.append(b)
+        torch.cuda.synchronize()
+        for _ in range(3):                     # the cascade's quiet mode, then its decision
+            for (hdr, ev, _), c, s, b in zip(batches, ctxs, streams, bufs):
+                c.check_device(models.MODEL_BANK, b[0].data_ptr(), len(hdr), b[1].data_ptr(), len(ev),
+                               b[2].data_ptr(), b[3].data_ptr(), None, None, stream=s.cuda_stream)
+        torch.cuda.synchronize()
+        for (hdr, ev, _), b in zip(batches, bufs):
+            st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr, ev, None, 0, 8, witness=False)
+            assert np.array_equal(b[2].cpu().numpy(), st_o)
+            assert np.array_equal(b[3].cpu().numpy().astype(np.uint64), nd_o.astype(np.uint64))
+    finally:
+        for c in ctxs[1:]:
+            c.close()
+
+
 def test_model0(ctx):
     rng = random.Random(99)
     hs = [histgen.wellformed_history(rng, "ticket", rng.randint(1, 6), 2) for _ in range(2000)]
