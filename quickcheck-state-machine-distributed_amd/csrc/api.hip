@@ -448,9 +448,6 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         c->auto_heavy = longs * kAutoFrac >= std::max<uint64_t>(c->probe_n_hist, 1);
         c->probe_pending = false;
     }
-    // (with the memo stage, a call that is not in heavy mode still sends the
-    // histories over the split budget to it: it searches most of them in far
-    // fewer nodes, and hands the rest to the split stage)
     // memo tables first: if the device cannot hold them, this context runs
     // without the memo stage (coop / spread take the heavy histories: the
     // same results, more work)
@@ -464,6 +461,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             HIP_TRY(c, hipMemsetAsync(c->mt, 0, c->mt_bytes, s), "memset memo tables");
         }
     }
+    // (with the memo stage, a call that is not in heavy mode still sends the
+    // histories over min(split budget, 512) nodes to it: it searches most of
+    // them in far fewer nodes, and hands the rest to the split stage)
     const uint64_t quiet0 = c->memo_stage ? std::min<uint64_t>(c->split_budget, kQuietBudget) : 0;
     const uint64_t budget0 = c->stage0_auto ? (c->auto_heavy ? kAutoBudget : quiet0) : c->stage0_budget;
     const bool probe = c->stage0_auto && !grp && !persistent && !c->probe_pending;
@@ -496,9 +496,14 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const uint64_t gwh = memo_w ? g_mw : heavy_w ? c->coop64_grid + (split ? 0 : kRedoGrid) : 0;
     const uint64_t gw = gw0 + gwh;
     const uint64_t n_part = g0r + g0b + gw + kStage1Grid + kStage2Grid + gsp + gfx;
-    // counters: [0] stage-1 list, [1] stage-2 list, [2] timed out, [3] unused,
-    //           [4] heavy list, [5] heavy queue head, [6] first failing history,
-    //           [7] giant list, [8..9] tasks per variant, [10..11] task queue heads
+    // counters (32 x u32, zeroed by prep_kernel; [6] = none):
+    //   [0] stage-0 defer list, [1] stage-1 defer list, [2] timed out, [3] never written,
+    //   [4] heavy list, [5] heavy queue head, [6] first failing history, [7] giant list,
+    //   [8..9] tasks per variant, [10..11] task queue heads, [12] persistent head,
+    //   [13..14] redo list / head, [16..17] spread ad, [18] spread head, [19] coop next,
+    //   [20] group next, [21] dynamic stage-0 head, [22] probe (long finished searches),
+    //   [23] stage-0w defer list, [24..26] stage-0w heavy list / coop64 next / redo list,
+    //   [27] stage-0r list, [28] straggler cuts
     const size_t off_cnt = 0;
     const size_t off_tot = 256;                                        // qsmd_totals
     const size_t off_l0 = 512;
