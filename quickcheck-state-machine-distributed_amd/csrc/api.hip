@@ -76,6 +76,10 @@ struct qsmd_ctx {
     unsigned long long* memo_stats = nullptr;   // diagnostic (memo_stats_ptr)
     uint64_t cut_k = 0;                // straggler cut: lanes still searching when a wave cuts them (0 = off)
     uint64_t cut_min = 16;             // ... after this many iterations
+    uint64_t split_xmemo = 1;          // split stage: exact-count memo for the giants' tasks
+    char* xm = nullptr;                // its table (kXMemoEntries x 128 B, epoch-tagged)
+    size_t xm_bytes = 0;
+    uint32_t xm_epoch = 0;
     uint64_t rerun_budget = 0;         // stage 0 budget before the lane re-run (stage 0r); 0 = none
     uint64_t stage0w = 1;              // 33..64-event histories in the compact kernel (else stage 1)
     uint64_t stage0w_budget = 32;      // stage 0w: nodes per history before the memo stage (coop64 without it; 0 = none)
@@ -123,6 +127,7 @@ constexpr uint64_t kTimingSlots = 1024;
 constexpr uint32_t kFrontierGrid = 256;  // split stage: one lane per giant history, grid-stride
 constexpr uint32_t kTaskGrid[SPLIT_VARIANTS] = {1024, 512};   // persistent task wavefronts
 constexpr uint32_t kCombineGrid = 64;
+constexpr uint64_t kXMemoEntries = 1ull << 21;   // split stage exact memo: 256 MB
 constexpr uint32_t kTaskCap = 1u << 19;  // tasks per variant per call (beyond: searched unsplit)
 constexpr uint32_t kSplitTarget = 256;   // tasks wanted per giant history
 constexpr uint32_t kSplitMaxTasks = 4096;
@@ -233,6 +238,7 @@ void qsmd_close(qsmd_ctx* c) {
     if (c->sx) (void)hipFree(c->sx);
     if (c->spt) (void)hipFree(c->spt);
     if (c->mt) (void)hipFree(c->mt);
+    if (c->xm) (void)hipFree(c->xm);
     if (c->memo) (void)hipFree(c->memo);
     if (c->io) (void)hipFree(c->io);
     for (auto e : c->ev)
@@ -315,6 +321,8 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->cut_k = value;
     } else if (n == "cut_min") {
         c->cut_min = std::min<uint64_t>(value, 0xFFFFFFFFull);
+    } else if (n == "split_xmemo") {
+        c->split_xmemo = value ? 1 : 0;
     } else if (n == "rerun_budget") {
         c->rerun_budget = value;
     } else if (n == "stage0w") {
@@ -829,6 +837,21 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             rc = memo_prepare(c, s, &p.memo);
             if (rc) return rc;
             p.memo_mask = c->memo_alloc - 1;
+        } else if (c->split_xmemo) {    // exact-count memo for the giants' tasks (the reference's counts)
+            const size_t need = (size_t)kXMemoEntries * 128;
+            if (c->xm_bytes < need) {
+                rc = grow(c, &c->xm, &c->xm_bytes, need);
+                if (rc) return rc;
+                HIP_TRY(c, hipMemsetAsync(c->xm, 0, c->xm_bytes, s), "memset exact memo");
+            }
+            if (((++c->xm_epoch) & 0xFFFFFFu) == 0u) {   // 24-bit tags wrapped: clear
+                HIP_TRY(c, hipMemsetAsync(c->xm, 0, c->xm_bytes, s), "memset exact memo");
+                ++c->xm_epoch;
+            }
+            p.memo = reinterpret_cast<unsigned long long*>(c->xm);
+            p.memo_mask = kXMemoEntries - 1;
+            p.memo_exact = 1;
+            p.memo_epoch = c->xm_epoch;
         }
         for (int v = 0; v < SPLIT_VARIANTS; ++v)
             HIP_TRY(c, launch_frontier(v, p, kFrontierGrid, s), "frontier launch");

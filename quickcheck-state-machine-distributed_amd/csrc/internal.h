@@ -124,8 +124,10 @@ struct SplitArgs {
     uint8_t* task_status;         // [SPLIT_VARIANTS][task_cap]
     uint64_t* task_nodes;
     uint8_t* task_witness;        // [SPLIT_VARIANTS][task_cap][kTaskWitness] or null
-    unsigned long long* memo;     // QSMD_FLAG_MEMO table (8 x u64 per entry) or null
+    unsigned long long* memo;     // QSMD_FLAG_MEMO table (8 x u64 per entry), the exact memo's, or null
     uint64_t memo_mask;           // entries - 1
+    uint32_t memo_exact;          // 1: exact-count memo (16 x u64 per entry, epoch-tagged)
+    uint32_t memo_epoch;          // exact memo: this call's tag (24 bits)
     uint32_t external_tasks;      // tasks given by the caller (qsmd_check_tasks)
 };
 
@@ -144,9 +146,9 @@ __host__ __device__ inline int combine_tasks(uint32_t term_status, uint64_t term
             *nodes_out = max_nodes && s == QSMD_STATUS_BUDGET ? max_nodes : tasks[i].top_before + sum;
             return s == QSMD_STATUS_SKIPPED ? QSMD_STATUS_SKIPPED : QSMD_STATUS_BUDGET;
         }
-        const uint64_t total = tasks[i].top_before + sum + nd[i];
-        if (total > limit) {
-            *nodes_out = limit;
+        uint64_t total;
+        if (__builtin_add_overflow(tasks[i].top_before + sum, nd[i], &total) || total > limit) {
+            *nodes_out = limit;              // (a count beyond 2^64 - 1: the budget of u64)
             return QSMD_STATUS_BUDGET;
         }
         sum += nd[i];
@@ -160,8 +162,8 @@ __host__ __device__ inline int combine_tasks(uint32_t term_status, uint64_t term
         *nodes_out = max_nodes ? max_nodes : term_nodes + sum;
         return QSMD_STATUS_BUDGET;
     }
-    const uint64_t total = term_nodes + sum;
-    if (total > limit) {
+    uint64_t total;
+    if (__builtin_add_overflow(term_nodes, sum, &total) || total > limit) {
         *nodes_out = limit;
         return QSMD_STATUS_BUDGET;
     }

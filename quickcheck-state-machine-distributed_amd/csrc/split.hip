@@ -85,6 +85,59 @@ struct MemoKey {
 struct Memo {
     unsigned long long* tab;
     uint64_t mask;
+    uint32_t epoch = 0;           // exact memo: the call's tag
+
+    // ---- exact-count memo (csrc/memo.hip's argument, shared by the split
+    // stage's lanes): 16 x u64 per entry = [tag | key 7 | count]; tag =
+    // epoch24 << 40 | (giant + 1) << 8 | hash7 << 1 | ready.  Writers claim an
+    // empty or stale (older epoch) slot by CAS, store key and count, then
+    // publish the ready bit with release; readers load the tag with acquire.
+    __device__ uint64_t xtag(const MemoKey& k, uint32_t id) const {
+        return ((uint64_t)(epoch & 0xFFFFFFu) << 40) | ((uint64_t)(id + 1u) << 8) | ((k.hash >> 56) & 0xFEull);
+    }
+    __device__ bool stale(uint64_t t) const { return t != 0 && (uint32_t)(t >> 40) != (epoch & 0xFFFFFFu); }
+    __device__ bool xlookup(const MemoKey& k, uint32_t id, uint64_t* count) const {
+        const uint64_t want = xtag(k, id);
+        for (int i = 0; i < kMemoProbe; ++i) {
+            unsigned long long* e = tab + ((k.hash + (uint64_t)i) & mask) * 16u;
+            const uint64_t t = __hip_atomic_load(e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == 0 || stale(t)) return false;   // an insert would have taken this slot
+            if (t != (want | 1ull)) continue;
+            bool eq = true;
+#pragma unroll
+            for (int q = 0; q < kMemoKey; ++q) eq = eq & (ld_sc1(e + 1 + q) == k.w[q]);
+            if (eq) {
+                *count = ld_sc1(e + 8);
+                return true;
+            }
+        }
+        return false;
+    }
+    __device__ void xinsert(const MemoKey& k, uint32_t id, uint64_t count) const {
+        const uint64_t want = xtag(k, id);
+        for (int i = 0; i < kMemoProbe; ++i) {
+            unsigned long long* e = tab + ((k.hash + (uint64_t)i) & mask) * 16u;
+            uint64_t t = ld_sc1(e);
+            while (t == 0 || stale(t)) {
+                const uint64_t old = atomicCAS(e, (unsigned long long)t, (unsigned long long)want);
+                if (old == t) {
+#pragma unroll
+                    for (int q = 0; q < kMemoKey; ++q) st_sc1(e + 1 + q, k.w[q]);
+                    st_sc1(e + 8, count);
+                    __hip_atomic_fetch_or(e, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    return;
+                }
+                t = old;                             // taken meanwhile: look at what is there now
+            }
+            if ((t | 1ull) == (want | 1ull)) {
+                if (!(t & 1ull)) return;             // being written (likely this very key)
+                bool eq = true;
+#pragma unroll
+                for (int q = 0; q < kMemoKey; ++q) eq = eq & (ld_sc1(e + 1 + q) == k.w[q]);
+                if (eq) return;                      // present (the same count: a function of the state)
+            }
+        }
+    }
 
     __device__ bool lookup(const MemoKey& k) const {
         for (int i = 0; i < kMemoProbe; ++i) {
@@ -136,6 +189,7 @@ struct GLds {
     uint32_t meta[MAXD][LANES];                         // j | pre-op model bits
     int64_t undo[BANK ? 1 : MAXD][LANES];               // Ticket: pre-op n
     int64_t bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][LANES];
+    uint64_t ent[MAXD][LANES];                          // exact memo: nodes counted on entering level d
 };
 
 template <typename MaskT> __device__ __forceinline__ uint64_t mask_lo(const MaskT& m) { return (uint64_t)m; }
@@ -325,24 +379,33 @@ struct GenDFS {
 
     // One DFS iteration.  Returns -1 (continue), kDescended (a node passed
     // its postcondition and was entered), or the final QSMD_STATUS_*.
-    template <bool MEMO>
+    // MEMO: 0 none, 1 QSMD_FLAG_MEMO (skip known-failing states: explored
+    // counts), 2 exact-count memo (add the recorded subtree count: the
+    // reference's counts)
+    template <int MEMO>
     __device__ int step(Lds& s, int lane, uint64_t limit, const Memo& memo, uint32_t id) {
         if (!Ops::any(cand)) {
             // no children: a leaf => True (any' []), the root => False (any []);
             // a subtree rooted at depth base > 0 is an inner node of the tree
             if (!found || depth == base) {
-                if constexpr (MEMO) {
+                if constexpr (MEMO != 0) {
                     if (found && depth > 0 && !skip_ins) {   // a task root that failed
                         const MemoKey k = key(id, s, lane);
-                        if (k.ok) memo.insert(k);
+                        if (k.ok) {
+                            if constexpr (MEMO == 2) memo.xinsert(k, id, nodes);   // the task counted its subtree
+                            else memo.insert(k);
+                        }
                     }
                 }
                 return (!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE;
             }
-            if constexpr (MEMO) {
+            if constexpr (MEMO != 0) {
                 if (!skip_ins) {
                     const MemoKey k = key(id, s, lane);      // this state failed
-                    if (k.ok) memo.insert(k);
+                    if (k.ok) {
+                        if constexpr (MEMO == 2) memo.xinsert(k, id, nodes - s.ent[depth - 1][lane]);
+                        else memo.insert(k);
+                    }
                 }
                 skip_ins = 0;
             }
@@ -368,9 +431,23 @@ struct GenDFS {
         if (post == POST_ERROR) return QSMD_STATUS_MODEL_ERROR;
         if (post == POST_FALSE) return -1;
         descend(j, ej, pm, r, s, lane);
-        if constexpr (MEMO) {
+        if constexpr (MEMO == 1) {
             const MemoKey k = key(id, s, lane);
             if (k.ok && memo.lookup(k)) {              // known to fail: skip the subtree
+                cand = MaskT{};
+                found = 1;
+                skip_ins = 1;
+            }
+        } else if constexpr (MEMO == 2) {
+            s.ent[depth - 1][lane] = nodes;
+            const MemoKey k = key(id, s, lane);
+            uint64_t c = 0, sum = 0;
+            if (k.ok && memo.xlookup(k, id, &c)) {     // searched before: its count, failed
+                if (__builtin_add_overflow(nodes, c, &sum) || sum > limit) {
+                    nodes = limit;                     // the budget falls inside that subtree
+                    return QSMD_STATUS_BUDGET;
+                }
+                nodes = sum;
                 cand = MaskT{};
                 found = 1;
                 skip_ins = 1;
@@ -421,7 +498,7 @@ __device__ int top_search(GenDFS<MODEL, MaskT, MAXEV, MAXPID, LANES>& d,
     count = 0;
     uint32_t iter = 0;
     for (;;) {
-        const int st = d.template step<false>(s, lane, limit, none, 0);
+        const int st = d.template step<0>(s, lane, limit, none, 0);
         if (st == kDescended) {
             if (d.depth == cut) {
                 if (out && count < max_count) {
@@ -481,6 +558,32 @@ __global__ __launch_bounds__(LANES) void frontier_search(SplitArgs p, uint32_t v
             p.giants[g] = G;
             continue;
         }
+        if (p.memo && p.memo_exact) {
+            // first the whole search in this lane with the exact memo, for a
+            // bounded number of iterations: most giants collapse to a few
+            // thousand states (their entries stay for the tasks if not)
+            Memo memo{p.memo, p.memo_mask};
+            memo.epoch = p.memo_epoch;
+            d.init(a, s, lane);
+            int st = -1;
+            uint32_t iter = 0;
+            const uint32_t cap = 64u * p.target;
+            while ((st = d.template step<2>(s, lane, limit, memo, g)) < 0 && ++iter < cap) {
+                if (sp_time_up(a, t0, iter)) {
+                    atomicOr(a.timed_out, 1u);
+                    st = QSMD_STATUS_BUDGET;
+                    break;
+                }
+            }
+            if (st >= 0) {                                         // decided here: no tasks
+                G.term_status = (uint32_t)st;
+                G.term_nodes = d.nodes;
+                if (a.witness && st == QSMD_STATUS_LINEARISABLE) d.path_to(a.witness + H.ev_off, d.n_ev, s, lane);
+                p.giants[g] = G;
+                continue;
+            }
+            // past the cap: the split below (top_search re-initialises the search)
+        }
         const uint32_t dmax = min(min(p.max_depth, (uint32_t)QSMD_SPLIT_MAX_DEPTH), d.n_ev / 2u);
         uint32_t cut = 1, count = 0;
         for (;; ++cut) {
@@ -512,7 +615,7 @@ __global__ __launch_bounds__(LANES) void frontier_search(SplitArgs p, uint32_t v
             const Memo none{nullptr, 0};
             d.init(a, s, lane);
             uint32_t iter = 0;
-            while ((st = d.template step<false>(s, lane, limit, none, 0)) < 0) {
+            while ((st = d.template step<0>(s, lane, limit, none, 0)) < 0) {
                 if (sp_time_up(a, t0, ++iter)) {
                     atomicOr(a.timed_out, 1u);
                     st = QSMD_STATUS_BUDGET;
@@ -541,8 +644,10 @@ __global__ __launch_bounds__(LANES) void task_search(SplitArgs p, uint32_t varia
     uint8_t* t_status = p.task_status + (uint64_t)variant * p.task_cap;
     uint64_t* t_nodes = p.task_nodes + (uint64_t)variant * p.task_cap;
     uint8_t* t_wit = p.task_witness ? p.task_witness + (uint64_t)variant * p.task_cap * kTaskWitness : nullptr;
-    const Memo memo{p.memo, p.memo_mask};
+    Memo memo{p.memo, p.memo_mask};
+    memo.epoch = p.memo_epoch;
     const bool use_memo = p.memo != nullptr;
+    const bool exact = use_memo && p.memo_exact;
     const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
 
@@ -583,9 +688,10 @@ __global__ __launch_bounds__(LANES) void task_search(SplitArgs p, uint32_t varia
                         iter = 0;
                         if (use_memo && T.depth > 0) {           // root state known to fail
                             const MemoKey k = d.key(g, s, lane);
-                            if (k.ok && memo.lookup(k)) {
+                            uint64_t c = 0;
+                            if (exact ? (k.ok && memo.xlookup(k, g, &c)) : (k.ok && memo.lookup(k))) {
                                 t_status[idx] = QSMD_STATUS_NONLINEARISABLE;
-                                t_nodes[idx] = 0;
+                                t_nodes[idx] = c;                // exact: the subtree's count
                                 busy = false;
                             }
                         }
@@ -594,8 +700,9 @@ __global__ __launch_bounds__(LANES) void task_search(SplitArgs p, uint32_t varia
             }
         }
         if (busy) {
-            int st = use_memo ? d.template step<true>(s, lane, limit, memo, g)
-                              : d.template step<false>(s, lane, limit, memo, g);
+            int st = exact ? d.template step<2>(s, lane, limit, memo, g)
+                     : use_memo ? d.template step<1>(s, lane, limit, memo, g)
+                                : d.template step<0>(s, lane, limit, memo, g);
             if (st < 0 && ((++iter & 1023u) == 0u)) {
                 const uint32_t mw = __hip_atomic_load(&p.giants[g].min_win, __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT);

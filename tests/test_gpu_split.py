@@ -217,3 +217,33 @@ def test_adversarial_ticket_memo(ctx, bug):
     assert int(st[0]) == int(st_o[0]) == (codec.STATUS_NONLIN if bug else codec.STATUS_LIN)
     if not bug:
         assert np.array_equal(w, w_o)
+
+
+@pytest.mark.parametrize("nc,no,status,nodes", [(6, 30, codec.STATUS_NONLIN, 88071120488677),
+                                                (4, 17, codec.STATUS_NONLIN, 923201),
+                                                (8, 40, codec.STATUS_BUDGET, None)])
+def test_adversarial_exhaustive_exact_memo(ctx, nc, no, status, nodes):
+    """Exhaustive mode (no QSMD_FLAG_MEMO): the split stage's exact-count memo
+    reports the reference's node count of adversarial histories no plain
+    search could count (pinned by the memoised transliteration,
+    tests/test_oracle.py); a count beyond 2^64 - 1 is a budget."""
+    h, e, _ = gen.adversarial_ticket(nc, no, bug=True)
+    st, nd, _, _ = ctx.check_arrays(models.MODEL_TICKET, h, e)
+    assert int(st[0]) == status
+    if nodes is not None:
+        assert int(nd[0]) == nodes
+
+
+@pytest.mark.parametrize("xmemo", [1, 0])
+@pytest.mark.parametrize("split", [64, 4096])
+def test_ticket_8x64_batch(ctx, xmemo, split):
+    """Batches of 8-client x 64-op TicketDispenser histories (128 events:
+    stage 2, a heavy tail into the split stage), with and without the split
+    stage's exact memo: the reference's verdicts, counts and witnesses."""
+    hdr, ev, _ = gen.generate_config("ticket_8x64", 0, 1500 if xmemo else 400)
+    ctx.set_param("split_xmemo", xmemo)
+    try:
+        with knobs(ctx, split=split):
+            _compare(ctx, models.MODEL_TICKET, hdr, ev, max_nodes=10**7)
+    finally:
+        ctx.set_param("split_xmemo", 1)

@@ -146,3 +146,70 @@ def test_wellformed_ref_matches_host_mirror():
         pids = rng.sample(["p0", "p1", "p2", "p3"], rng.randint(1, 4))
         err = wellformed(pids, h)
         assert wellformed_ref.wellformed(pids, h) == (None if err is None else (err.kind, tuple(err.args)))
+
+
+def _memo_count(transition, postcondition, model0, es):
+    """Exact reference node count with a state memo (the argument of
+    DESIGN.md §4.1): linearise_lists' own forest and models, a failed
+    subtree's count reused for a repeated (remaining history, model)."""
+    import linearise_lists as LL
+    memo = {}
+
+    def sub(model, es2):
+        k = (tuple(es2), model if not isinstance(model, dict) else tuple(sorted(model.items())))
+        if k in memo:
+            return False, memo[k]
+        cnt, first = 0, True
+        for node in LL.interleavings(es2):
+            first = False
+            ok, c = step(model, node)
+            cnt += c
+            if ok:
+                return True, cnt
+        if first:
+            return True, 0
+        memo[k] = cnt
+        return False, cnt
+
+    def step(model, node):
+        _pid, inv, resp, es2 = node
+        if not postcondition(model, inv, resp):
+            return False, 1
+        ok, c = sub(transition(transition(model, ("L", inv)), ("R", resp)), es2)
+        return ok, 1 + c
+
+    total = 0
+    for node in LL.interleavings(es):
+        ok, c = step(model0, node)
+        total += c
+        if ok:
+            return "lin", total
+    return "nonlin", total
+
+
+def test_memo_count_equals_plain_count_and_pins_large_adversarial_counts():
+    """The memoised count equals the plain transliteration's on the 4x17
+    adversarial history (923201 nodes), and pins the exact counts the GPU's
+    exact memo reports beyond any plain search: 6x30 -> 88071120488677,
+    8x40 -> 36212384984955121261601 (> 2^64: a budget on the GPU)."""
+    import sys
+    sys.setrecursionlimit(100000)
+    import linearise_lists as LL
+    from qsmd import codec, gen, models
+
+    def hist(nc, no):
+        h, e, _ = gen.adversarial_ticket(nc, no, bug=True)
+
+        class B:
+            pass
+        b = B()
+        b.hdr, b.events, b.model = h, e, models.TICKET
+        b.pid_maps, b.account_maps = {0: {0: 0}}, {0: {}}
+        return codec.decode_history(b, 0)
+
+    h = hist(4, 17)
+    assert _memo_count(LL.ticket_transition, LL.ticket_postcondition, None, h) == ("nonlin", 923201)
+    assert LL.linearisable(LL.ticket_transition, LL.ticket_postcondition, None, h)[:2] == ("nonlin", 923201)
+    assert _memo_count(LL.ticket_transition, LL.ticket_postcondition, None, hist(6, 30)) == ("nonlin", 88071120488677)
+    assert _memo_count(LL.ticket_transition, LL.ticket_postcondition, None, hist(8, 40)) == \
+        ("nonlin", 36212384984955121261601)
