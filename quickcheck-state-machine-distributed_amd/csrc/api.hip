@@ -127,7 +127,7 @@ constexpr uint64_t kTimingSlots = 1024;
 constexpr uint32_t kFrontierGrid = 256;  // split stage: one lane per giant history, grid-stride
 constexpr uint32_t kTaskGrid[SPLIT_VARIANTS] = {1024, 512};   // persistent task wavefronts
 constexpr uint32_t kCombineGrid = 64;
-constexpr uint64_t kXMemoEntries = 1ull << 21;   // split stage exact memo: 256 MB
+constexpr uint64_t kXMemoEntries = 1ull << 22;   // split stage exact memo: 512 MB (shared by all giants of a call)
 constexpr uint32_t kTaskCap = 1u << 19;  // tasks per variant per call (beyond: searched unsplit)
 constexpr uint32_t kSplitTarget = 256;   // tasks wanted per giant history
 constexpr uint32_t kSplitMaxTasks = 4096;

@@ -90,8 +90,11 @@ struct Memo {
     // ---- exact-count memo (csrc/memo.hip's argument, shared by the split
     // stage's lanes): 16 x u64 per entry = [tag | key 7 | count]; tag =
     // epoch24 << 40 | (giant + 1) << 8 | hash7 << 1 | ready.  Writers claim an
-    // empty or stale (older epoch) slot by CAS, store key and count, then
-    // publish the ready bit with release; readers load the tag with acquire.
+    // empty or stale (older epoch) slot by CAS, store key and count with
+    // agent-scope (sc1) stores, drain them, then set the ready bit; readers use
+    // sc1 loads (the protocol of the QSMD_FLAG_MEMO table and the spread
+    // stage's task records) and take a count only under a ready, matching tag
+    // and all seven key words.
     __device__ uint64_t xtag(const MemoKey& k, uint32_t id) const {
         return ((uint64_t)(epoch & 0xFFFFFFu) << 40) | ((uint64_t)(id + 1u) << 8) | ((k.hash >> 56) & 0xFEull);
     }
@@ -100,7 +103,7 @@ struct Memo {
         const uint64_t want = xtag(k, id);
         for (int i = 0; i < kMemoProbe; ++i) {
             unsigned long long* e = tab + ((k.hash + (uint64_t)i) & mask) * 16u;
-            const uint64_t t = __hip_atomic_load(e, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t t = ld_sc1(e);
             if (t == 0 || stale(t)) return false;   // an insert would have taken this slot
             if (t != (want | 1ull)) continue;
             bool eq = true;
@@ -124,7 +127,8 @@ struct Memo {
 #pragma unroll
                     for (int q = 0; q < kMemoKey; ++q) st_sc1(e + 1 + q, k.w[q]);
                     st_sc1(e + 8, count);
-                    __hip_atomic_fetch_or(e, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // key and count land before the bit
+                    __hip_atomic_fetch_or(e, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     return;
                 }
                 t = old;                             // taken meanwhile: look at what is there now
@@ -612,10 +616,14 @@ __global__ __launch_bounds__(LANES) void frontier_search(SplitArgs p, uint32_t v
             G.n_tasks = count;
             G.depth = cut;
         } else {
-            const Memo none{nullptr, 0};
+            // no task slots left: the whole search here (with the exact memo if on)
+            Memo memo{p.memo, p.memo_mask};
+            memo.epoch = p.memo_epoch;
+            const bool exact = p.memo && p.memo_exact;
             d.init(a, s, lane);
             uint32_t iter = 0;
-            while ((st = d.template step<0>(s, lane, limit, none, 0)) < 0) {
+            while ((st = exact ? d.template step<2>(s, lane, limit, memo, g)
+                               : d.template step<0>(s, lane, limit, memo, 0)) < 0) {
                 if (sp_time_up(a, t0, ++iter)) {
                     atomicOr(a.timed_out, 1u);
                     st = QSMD_STATUS_BUDGET;
