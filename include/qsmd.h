@@ -211,7 +211,7 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *   "split_budget", "stage0_budget", "stage0_grid"  as the setters below */
 int qsmd_set_param(qsmd_ctx* ctx, const char* name, uint64_t value);
 
-/* Tuning knob: node budget of the per-lane searches (default 4096).  A
+/* Tuning knob: node budget of the per-lane searches (default 1024).  A
  * history whose search needs more nodes is handed to the split stage, which
  * searches it again with many lanes (see "Split search" below).  0 disables
  * the split stage.  Results are unchanged. */

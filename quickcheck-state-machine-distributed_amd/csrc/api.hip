@@ -55,7 +55,7 @@ struct qsmd_ctx {
     uint8_t* wf_rank_host = nullptr;   // wellformed: pid rank table (pinned) and its device copy
     char* wf_rank_dev = nullptr;
     size_t wf_rank_bytes = 0;
-    uint64_t split_budget = 4096;      // per-lane node budget before the split stage (0 = none)
+    uint64_t split_budget = 1024;      // per-lane node budget before the split stage (0 = none)
     uint64_t stage0_persistent = 0;    // > 0: stage 0 = persistent refill_search (direct) with this grid
     uint64_t refill_min = 8;           // refill kernels: idle lanes before a wavefront refills
     uint64_t spread_budget = 1024;     // spread stage: nodes a task searches before it splits

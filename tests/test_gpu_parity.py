@@ -160,6 +160,7 @@ def test_generated_configs(ctx, name, n, budget, kernel):
         st, nd, _ = _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
     finally:
         ctx.set_stage0_budget(0)
+        ctx.set_param("stage0_auto", 1)
         ctx.set_param("stage0_kernel", 0)
         ctx.set_param("stage0_dynamic", 0)
         ctx.set_param("stage0_grid", 65536)
@@ -206,6 +207,7 @@ def test_memo_stage(ctx, name, n, budget, max_nodes, entries):
     finally:
         ctx.set_param("memo_lane_entries", 128)
         ctx.set_stage0_budget(0)
+        ctx.set_param("stage0_auto", 1)
         ctx.set_param("stage0w_budget", 32)
         ctx.set_param("stage0_auto", 1)
 
@@ -261,7 +263,7 @@ def test_memo_stage_handoff(ctx, split_budget):
             for _ in range(2):
                 _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
     finally:
-        ctx.set_param("split_budget", 4096)
+        ctx.set_param("split_budget", 1024)
         ctx.set_param("stage0_auto", 1)
 
 
@@ -356,6 +358,7 @@ def test_budget(ctx):
                     assert (nd <= budget).all()
             finally:
                 ctx.set_stage0_budget(0)
+                ctx.set_param("stage0_auto", 1)
                 ctx.set_param("stage0w_budget", 32)
                 ctx.set_param("memo_stage", 1)
 
@@ -383,6 +386,7 @@ def test_early_exit_batch(ctx, name, shift):
                                           device.QSMD_FLAG_EARLY_EXIT_BATCH, max_nodes=10**7)
     finally:
         ctx.set_stage0_budget(0)
+        ctx.set_param("stage0_auto", 1)
     assert np.array_equal(st[:cut + 1], st_o[:cut + 1]) and np.array_equal(nd[:cut + 1], nd_o[:cut + 1])
     assert (st[cut + 1:] == codec.STATUS_SKIPPED).all() and (nd[cut + 1:] == 0).all()
     assert tot["skipped"] == max(0, len(hdr) - cut - 1)
@@ -542,3 +546,4 @@ def test_adaptive_cascade(ctx):
             _compare(ctx, models.MODEL_BANK, hdr, ev)
     finally:
         ctx.set_stage0_budget(0)
+        ctx.set_param("stage0_auto", 1)

@@ -22,7 +22,7 @@ from test_gpu_parity import _compare
 
 pytestmark = pytest.mark.gpu
 
-DEFAULT_SPLIT = 4096
+DEFAULT_SPLIT = 1024
 EXH = device.QSMD_FLAG_EXHAUSTIVE
 MEMO = device.QSMD_FLAG_MEMO
 
@@ -37,7 +37,7 @@ def knobs(ctx, split=None, stage0=None):
         yield
     finally:
         ctx.set_split_budget(DEFAULT_SPLIT)
-        ctx.set_stage0_budget(0)
+        ctx.set_param("stage0_auto", 1)
 
 
 @pytest.mark.parametrize("split", [1, 16, 200])

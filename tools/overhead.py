@@ -35,4 +35,4 @@ for name, kv in (("default", {}), ("no_split", {"split_budget": 0}), ("no_0w", {
     print(json.dumps({"variant": name, "stage0_us": round(1e3 * float(np.median(s0)), 2),
                       "call_us": round(1e3 * float(np.median(call)), 2)}), flush=True)
     for k in kv:
-        ctx.set_param(k, {"split_budget": 4096, "stage0w": 1, "memo_stage": 1}[k])
+        ctx.set_param(k, {"split_budget": 1024, "stage0w": 1, "memo_stage": 1}[k])

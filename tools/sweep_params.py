@@ -17,7 +17,7 @@ import torch  # noqa: E402
 
 from qsmd import device, gen  # noqa: E402
 
-DEFAULTS = {"stage0_persistent_grid": 0, "refill_min": 8, "split_budget": 4096, "stage0_budget": 0,
+DEFAULTS = {"stage0_persistent_grid": 0, "refill_min": 8, "split_budget": 1024, "stage0_auto": 1,
             "stage0_grid": 65536}
 
 
