@@ -94,7 +94,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--split-budget", type=int, default=None,
                     help="per-lane node budget before the split stage (library default if unset)")
-    ap.add_argument("--stage0-budget", type=int, default=None)
+    ap.add_argument("--stage0-budget", type=int, default=None,
+                    help="fixed stage-0 node budget (the rest go to the memo stage); default 32 with calls in "
+                         "flight (the next batch hides the memo stage: +1.5-3%% on configs 1, 2, 3, 5, "
+                         "tools/gpu/inflight_budget2.sh), the adaptive cascade one call at a time; -1 = adaptive")
     ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")
     ap.add_argument("--inflight", type=int, default=0,
                     help="calls in flight (one context + stream each): the next step's search overlaps the tail of "
@@ -142,11 +145,12 @@ def main():
     # full search of the batch; a slot's steps are ordered on its stream.
     S = args.inflight if args.inflight > 0 else (2 if use_dist else 3)
     ctxs = [ctx] + [device.Context(local) for _ in range(S - 1)]
+    budget0 = args.stage0_budget if args.stage0_budget is not None else (32 if S > 1 else -1)
     for c in ctxs:
         if args.split_budget is not None:
             c.set_split_budget(args.split_budget)
-        if args.stage0_budget is not None:
-            c.set_stage0_budget(args.stage0_budget)
+        if budget0 >= 0:
+            c.set_stage0_budget(budget0)
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
@@ -229,7 +233,10 @@ def main():
 
     # roofline of the dominant kernel (stage 0 search), rank-local
     s0_mean = float(np.mean(s0_ms)) if len(s0_ms) else float("nan")
-    a_bytes = alg_bytes(hdr, nd)
+    # (with a fixed stage-0 budget the kernel stops a history at that many
+    # nodes and the memo stage searches it again: stage 0's own node work is
+    # min(nodes, budget) per history)
+    a_bytes = alg_bytes(hdr, np.minimum(nd, budget0) if budget0 > 0 else nd)
     achieved = a_bytes / (s0_mean * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic):
@@ -247,7 +254,7 @@ def main():
         "config": {"workload": args.config, "histories_per_gpu": n,
                    "clients": cfg["n_clients"], "ops": cfg["n_ops"],
                    "events_per_history": 2 * cfg["n_ops"], "parallelism": f"shard{world}", "calls_in_flight": S,
-                   "mode": "memo" if args.memo else "exhaustive"},
+                   "stage0_budget": budget0 if budget0 >= 0 else "adaptive", "mode": "memo" if args.memo else "exhaustive"},
         "nodes_per_sec": nodes_total * args.steps / elapsed,
         "verdicts": {"checked": int(tot[0]), "linearisable": int(tot[1]),
                      "nonlinearisable": int(tot[2]), "model_errors": int(tot[3]),
