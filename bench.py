@@ -95,9 +95,11 @@ def main():
     ap.add_argument("--split-budget", type=int, default=None,
                     help="per-lane node budget before the split stage (library default if unset)")
     ap.add_argument("--stage0-budget", type=int, default=None,
-                    help="fixed stage-0 node budget (the rest go to the memo stage); default 32 with calls in "
-                         "flight (the next batch hides the memo stage: +1.5-3%% on configs 1, 2, 3, 5, "
-                         "tools/gpu/inflight_budget2.sh), the adaptive cascade one call at a time; -1 = adaptive")
+                    help="fixed stage-0 node budget (the rest go to the memo stage); default 40 with calls in "
+                         "flight (the next batch hides the memo stage; tools/gpu/inflight_budget*.sh, "
+                         "profiles/r01/v7/inflight_budget_sweep.json), the adaptive cascade one call at a time; -1 = adaptive")
+    ap.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
+                    help="qsmd_set_param on every context (tuning; repeatable)")
     ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")
     ap.add_argument("--inflight", type=int, default=0,
                     help="calls in flight (one context + stream each): the next step's search overlaps the tail of "
@@ -145,12 +147,15 @@ def main():
     # full search of the batch; a slot's steps are ordered on its stream.
     S = args.inflight if args.inflight > 0 else (2 if use_dist else 3)
     ctxs = [ctx] + [device.Context(local) for _ in range(S - 1)]
-    budget0 = args.stage0_budget if args.stage0_budget is not None else (32 if S > 1 else -1)
+    budget0 = args.stage0_budget if args.stage0_budget is not None else (40 if S > 1 else -1)
     for c in ctxs:
         if args.split_budget is not None:
             c.set_split_budget(args.split_budget)
         if budget0 >= 0:
             c.set_stage0_budget(budget0)
+        for kv in args.param:
+            name, value = kv.split("=")
+            c.set_param(name, int(value))
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
