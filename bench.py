@@ -86,8 +86,8 @@ def cpu_baseline(hdr, ev, model_id, target_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="bank_4x16", choices=sorted(gen.CONFIGS))
     ap.add_argument("--n-hist", type=int, default=1_000_000, help="histories per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
