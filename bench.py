@@ -104,6 +104,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=0,
                     help="calls in flight (one context + stream each): the next step's search overlaps the tail of "
                          "the previous one; 0 = 3 on one GPU, 2 with RCCL (its stream takes one of the 4 hardware queues)")
+    ap.add_argument("--ar-rounds", type=int, default=16,
+                    help="rounds of in-flight steps whose counters one RCCL all-reduce carries (N > 1)")
     ap.add_argument("--device-gen", action="store_true",
                     help="generate the batch on the GPU (qsmd_gen_batch_device; same histories as the host generator)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -160,10 +162,13 @@ def main():
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
             for _ in range(S)]
-    # counters: [round parity][slot][8]; the S steps of a round are all-reduced
-    # together (one bucketed RCCL all-reduce per round, on its own stream,
-    # overlapping the next round; a row is reused two rounds later, after it)
-    tot = torch.zeros(2, S, 8, dtype=torch.int64, device=dev)
+    # counters: [block parity][step of the block][8]; a block is R rounds of S
+    # steps (--ar-rounds), all-reduced together (one bucketed RCCL all-reduce
+    # per block, overlapping the next block; a row is reused two blocks later,
+    # after it)
+    R = max(1, args.ar_rounds)
+    B = R * S
+    tot = torch.zeros(2, B, 8, dtype=torch.int64, device=dev)
     # (the round's all-reduce runs on the last slot's stream: RCCL adds its own
     # stream, and more streams than hardware queues serialise each other)
     comm = streams[S - 1] if use_dist else None
@@ -174,34 +179,34 @@ def main():
     def step():
         k = k_step[0]
         k_step[0] += 1
-        i, par = k % S, (k // S) % 2
+        i, row, par = k % S, k % B, (k // B) % 2
         d_st_i, d_nd_i = outs[i]
         with torch.cuda.stream(streams[i]):
             if done[par] is not None:
                 streams[i].wait_event(done[par])
             ctxs[i].check_device(model_id, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st_i.data_ptr(),
-                                 d_nd_i.data_ptr(), None, tot[par, i].data_ptr(), flags=flags,
+                                 d_nd_i.data_ptr(), None, tot[par, row].data_ptr(), flags=flags,
                                  stream=streams[i].cuda_stream)
-        if do_ar and (i == S - 1):        # the round is enqueued: its counters all-reduced together
+        if do_ar and row == B - 1:        # the block is enqueued: its counters all-reduced together
             for st_ in streams[:-1]:
                 comm.wait_stream(st_)
             with torch.cuda.stream(comm):
                 dist.all_reduce(tot[par], op=dist.ReduceOp.SUM)
                 done[par] = torch.cuda.Event()
                 done[par].record(comm)
-        return i, par
+        return row, par
 
     def drain():
-        if k_step[0] % S:                 # a partial last round: reduce it, start the next one fresh
+        if k_step[0] % B:                 # a partial last block: reduce it, start the next one fresh
             if do_ar:
-                par = ((k_step[0] - 1) // S) % 2
+                par = ((k_step[0] - 1) // B) % 2
                 for st_ in streams[:-1]:
                     comm.wait_stream(st_)
                 with torch.cuda.stream(comm):
                     dist.all_reduce(tot[par], op=dist.ReduceOp.SUM)
                     done[par] = torch.cuda.Event()
                     done[par].record(comm)
-            k_step[0] = (k_step[0] + S - 1) // S * S
+            k_step[0] = (k_step[0] + B - 1) // B * B
 
     for _ in range(args.warmup):
         step()
@@ -226,7 +231,7 @@ def main():
         elapsed = float(e.item())
 
     s0_ms, call_ms = ctx.timing_read()
-    d_st, d_nd = outs[last[0]]
+    d_st, d_nd = outs[last[0] % S]
     st = d_st.cpu().numpy()
     nd = d_nd.cpu().numpy()
     tot = tot[last[1], last[0]].cpu().numpy()   # global totals of the last step
@@ -259,7 +264,8 @@ def main():
         "config": {"workload": args.config, "histories_per_gpu": n,
                    "clients": cfg["n_clients"], "ops": cfg["n_ops"],
                    "events_per_history": 2 * cfg["n_ops"], "parallelism": f"shard{world}", "calls_in_flight": S,
-                   "stage0_budget": budget0 if budget0 >= 0 else "adaptive", "mode": "memo" if args.memo else "exhaustive"},
+                   "stage0_budget": budget0 if budget0 >= 0 else "adaptive",
+                   "allreduce_every_steps": B if use_dist else None, "mode": "memo" if args.memo else "exhaustive"},
         "nodes_per_sec": nodes_total * args.steps / elapsed,
         "verdicts": {"checked": int(tot[0]), "linearisable": int(tot[1]),
                      "nonlinearisable": int(tot[2]), "model_errors": int(tot[3]),
