@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define QSMD_ABI_VERSION 1u
+#define QSMD_ABI_VERSION 2u
 
 /* ---------------------------------------------------------------- layout */
 
@@ -154,11 +154,20 @@ typedef struct qsmd_ctx qsmd_ctx;
 #define QSMD_ERR_NOMEM      -3
 #define QSMD_ERR_UNSUPPORTED -4
 
-/* Bind a context to one HIP device (one process per GPU). */
+/* Bind a context to one HIP device (one process per GPU).  SURVEY.md §8b
+ * proposed a device mask; a context serves exactly one device instead, and a
+ * process drives several GPUs with one context per device. */
 int  qsmd_open(qsmd_ctx** out, int device);
 void qsmd_close(qsmd_ctx* ctx);
 const char* qsmd_last_error(const qsmd_ctx* ctx);
 uint32_t qsmd_abi_version(void);
+
+/* Threading and streams.  Every entry point of one context serialises on the
+ * context's mutex, and the check calls of one context are ordered: a call on
+ * a stream other than the previous call's first waits (on the device) for
+ * that call, because they share the context's device workspace.  Calls that
+ * should overlap use one context each (bench.py keeps calls in flight that
+ * way).  Contexts share no device state. */
 
 /* Check a batch held in HOST memory (the drop-in for one call per history;
  * n_hist = 1 is valid).  Buffers are copied in and out; the library keeps no
@@ -172,9 +181,10 @@ int qsmd_check_batch(qsmd_ctx* ctx, uint32_t model_id,
                      uint8_t* witness_out, qsmd_totals* totals_out);
 
 /* Same, with every buffer already resident in device memory (HBM) and work
- * enqueued on `stream` (a hipStream_t, NULL = the context's stream).
- * totals_dev (device, may be NULL) receives the qsmd_totals of the batch.
- * Asynchronous: synchronise the stream before reading outputs. */
+ * enqueued on `stream` (a hipStream_t, NULL = the context's stream): four
+ * kernel launches, no host round trip.  totals_dev (device, may be NULL)
+ * receives the qsmd_totals of the batch.  Asynchronous: synchronise the
+ * stream before reading outputs. */
 int qsmd_check_batch_device(qsmd_ctx* ctx, uint32_t model_id,
                             const qsmd_hdr* hdr_dev, uint64_t n_hist,
                             const qsmd_event* events_dev, uint64_t n_events,
@@ -194,36 +204,45 @@ int qsmd_set_time_limit_ms(qsmd_ctx* ctx, uint64_t ms);
  * Default 65536.  Does not change any result. */
 int qsmd_set_stage0_grid(qsmd_ctx* ctx, uint64_t max_blocks);
 
-/* Tuning knob: node budget of the first search stage (default 0 = none).  A history
- * whose search needs more nodes is searched again, from scratch, by a
- * persistent stage whose idle lanes pull further histories, so one long
- * search does not hold 63 idle lanes.  0 disables.  Results are unchanged. */
+/* Tuning knob: node budget of the first search stage (default 32; 0 = none).
+ * A history whose search needs more nodes is searched again, from the root,
+ * by the heavy stage (one wavefront per history), so one long search does
+ * not hold 63 idle lanes.  Results are unchanged. */
 int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
 
 /* Tuning knobs by name (none changes a result):
- *   "stage0_persistent_grid"  > 0: the first stage runs as persistent
- *                             wavefronts whose lanes each pull the next
- *                             history as soon as they finish (this many
- *                             workgroups); 0 (default): 64 histories per
- *                             wavefront, staged together
- *   "refill_min"              idle lanes before a persistent wavefront
- *                             refills (1..64, default 8)
- *   "split_budget", "stage0_budget", "stage0_grid"  as the setters below */
+ *   "stage0_budget"     as qsmd_set_stage0_budget
+ *   "stage0w_budget"    the same for 33..64-event histories (default 32)
+ *   "stage0_grid"       as qsmd_set_stage0_grid
+ *   "split_budget"      as qsmd_set_split_budget
+ *   "split_xmemo"       1 (default): the giant stage's exact-count memo
+ *   "wave_budget"       heavy stage: nodes a lane's task counts before it
+ *                       may hand the rest to idle lanes (default 16)
+ *   "wave_grid"         heavy stage workgroups (0 = 3 per CU)
+ *   "giant_grid"        giant stage workgroups (0 = 2 per CU)
+ *   "heavy_mode"        0: one wavefront per heavy history; 1: one lane per
+ *                       heavy history with a private HBM memo table; 2
+ *                       (default): lane mode while the last finished call
+ *                       sent more than "wave_max" (default 16384) histories
+ *                       to the heavy stage
+ *   "memo_grid", "memo_lane_entries"  lane mode: workgroups, entries per lane */
 int qsmd_set_param(qsmd_ctx* ctx, const char* name, uint64_t value);
 
-/* Tuning knob: node budget of the per-lane searches (default 1024).  A
- * history whose search needs more nodes is handed to the split stage, which
- * searches it again with many lanes (see "Split search" below).  0 disables
- * the split stage.  Results are unchanged. */
+/* Tuning knob (default 1024): histories the compact stages cannot hold go to
+ * the giant stage, which first searches each one in a lane for 16 x this
+ * many iterations and otherwise splits it over many lanes (see "Split
+ * search" below); the heavy stage hands it a history after 64 x this many
+ * iterations.  0 disables the split (every search runs to its end in one
+ * lane or wavefront).  Results are unchanged. */
 int qsmd_set_split_budget(qsmd_ctx* ctx, uint64_t nodes);
 
-/* QSMD_FLAG_MEMO: the split stage keeps a table in HBM of search states
+/* QSMD_FLAG_MEMO: the giant stage keeps a table in HBM of search states
  * (remaining events, model) known to fail, shared by every lane searching the
  * same history, and prunes a subtree whose root state is in it.  Verdicts
- * and witnesses are unchanged; node counts become "nodes explored" (fewer
- * than the reference's, and not reproducible from run to run).  Capacity in
- * entries of 64 B, a power of two (default 1 << 22 = 256 MiB, allocated on
- * first use). */
+ * and witnesses are unchanged; node counts of the giant stage's histories
+ * become "nodes explored" (fewer than the reference's, and not reproducible
+ * from run to run).  Capacity in entries of 64 B, a power of two (default
+ * 1 << 22 = 256 MiB, allocated on first use). */
 int qsmd_set_memo_capacity(qsmd_ctx* ctx, uint64_t entries);
 
 /* ----------------------------------------------------------- split search
@@ -325,19 +344,6 @@ int qsmd_wellformed_batch_device(qsmd_ctx* ctx, const qsmd_hdr* hdr_dev, uint64_
                                  const uint8_t* pids, uint32_t n_pids, qsmd_wf* out_dev,
                                  void* stream);
 
-/* Diagnostic: when stamps_dev (device memory, 8 x u64 per stage-0
- * workgroup) is non-NULL, stage 0 runs an instrumented build that records
- * per-workgroup s_memtime totals of its phases (staging, search, output,
- * groups processed) and its residency (s_memrealtime at start and end,
- * HW_ID, XCC_ID).  NULL restores the production kernel. */
-int qsmd_diag_stamps(qsmd_ctx* ctx, void* stamps_dev);
-
-/* Diagnostic: the spread stage (dynamic split of the histories over the
- * stage-0 node budget) of the most recent call: out4[0] = histories it
- * searched, [1] = tasks, [2] = nodes explored (speculation included),
- * [3] = sum of their reference node counts.  Synchronises the device. */
-int qsmd_spread_stats(qsmd_ctx* ctx, uint64_t* out4);
-
 /* Device time (ms, HIP events on the launch stream) of the search kernels of
  * the most recent check call, measured once that stream has completed. */
 int qsmd_last_kernel_ms(qsmd_ctx* ctx, float* ms_out);
@@ -348,6 +354,11 @@ int qsmd_last_kernel_ms(qsmd_ctx* ctx, float* ms_out);
 int qsmd_timing_reset(qsmd_ctx* ctx);
 int qsmd_timing_read(qsmd_ctx* ctx, float* stage0_ms, float* call_ms, uint64_t max,
                      uint64_t* n_out);
+
+/* Diagnostic: out4 = [histories stage 0 passed to stage 0w, heavy histories
+ * of stage 0, heavy histories of stage 0w, giants] of the most recent check
+ * call (waits for it). */
+int qsmd_probe_read(qsmd_ctx* ctx, uint32_t* out4);
 
 #ifdef __cplusplus
 }

@@ -575,10 +575,6 @@ struct LaneDFS {
     }
 };
 
-__device__ __forceinline__ bool time_up(const SearchArgs& a, uint64_t t0, uint32_t& iter) {
-    return a.time_limit && ((++iter & 1023u) == 0u) && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit;
-}
-
 // Wave-aggregated append of h to list (one atomic per wavefront).
 __device__ __forceinline__ void wave_append(bool pred, uint32_t h, uint32_t* list, uint32_t* count, int lane) {
     const uint64_t dm = __ballot(pred);
@@ -603,20 +599,20 @@ struct Counters {
         budget += status == QSMD_STATUS_BUDGET;
         nodes += n;
     }
-    __device__ __forceinline__ void flush(unsigned long long* partials, int lane) const {
+    // the wavefront's counts into its bucket (lane k adds count k: one
+    // atomic instruction per wavefront)
+    __device__ __forceinline__ void flush(unsigned long long* buckets, int lane) const {
         const uint64_t t_lin = wave_sum64(lin), t_non = wave_sum64(nonlin), t_err = wave_sum64(err),
                        t_enc = wave_sum64(enc), t_bud = wave_sum64(budget), t_nodes = wave_sum64(nodes);
-        if (lane == 0) {
-            unsigned long long* p = partials + (uint64_t)blockIdx.x * T_N;
-            p[T_CHECKED] = t_lin + t_non + t_err;
-            p[T_LIN] = t_lin;
-            p[T_NONLIN] = t_non;
-            p[T_ERR] = t_err;
-            p[T_ENC] = t_enc;
-            p[T_BUDGET] = t_bud;
-            p[T_SKIPPED] = 0;
-            p[T_NODES] = t_nodes;
-        }
+        const uint64_t v = lane == T_CHECKED ? t_lin + t_non + t_err
+                         : lane == T_LIN     ? t_lin
+                         : lane == T_NONLIN  ? t_non
+                         : lane == T_ERR     ? t_err
+                         : lane == T_ENC     ? t_enc
+                         : lane == T_BUDGET  ? t_bud
+                         : lane == T_NODES   ? t_nodes
+                                             : 0ull;
+        bucket_add(buckets, blockIdx.x, (uint32_t)lane, v);
     }
 };
 

@@ -50,10 +50,6 @@ struct MemoKey {
     bool ok;
 };
 
-struct MemoStats {
-    uint64_t iters, hits, inserts, max_iters;
-};
-
 __device__ __forceinline__ uint32_t mix32(uint32_t h) {
     h ^= h >> 16;
     h *= 0x7FEB352Du;
@@ -125,8 +121,7 @@ __device__ __forceinline__ void memo_insert(uint32_t* tab, const MemoKey<MODEL, 
 template <uint32_t MODEL, class G, int MODE>
 __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* evc,
                                          int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* tab,
-                                         uint32_t h, uint32_t epoch, uint32_t mask, uint32_t* entry, bool& skip,
-                                         uint32_t min_rem, MemoStats& ms) {
+                                         uint32_t h, uint32_t epoch, uint32_t mask, uint32_t* entry, bool& skip) {
     using M = typename G::M;
     const bool empty = d.cand == (M)0;
     const bool term = empty & ((d.found == 0u) | (d.depth == d.base));
@@ -135,14 +130,10 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     if (empty & !term) {
         // leaving the node at depth d.depth: its subtree was searched to the end and failed
         // (counts kept mod 2^32: exact while the running count is below 2^32)
-        // (small subtrees -- at most min_rem events left -- are cheaper to search than to look up)
-        if (!skip && d.nodes <= 0xFFFFFFFFull && (uint32_t)__builtin_popcountll((uint64_t)d.rem) > min_rem) {
+        if (!skip && d.nodes <= 0xFFFFFFFFull) {
             const uint32_t cnt = (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES];
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
-            if (k.ok) {
-                memo_insert<MODEL, G>(tab, k, h, cnt);
-                ++ms.inserts;
-            }
+            if (k.ok) memo_insert<MODEL, G>(tab, k, h, cnt);
         }
         skip = false;
         const uint32_t j = d.template undo<C_LANES, MODE>(evc, s_bal, lane);
@@ -154,11 +145,9 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
         status = d.template try_next<C_LANES, MODE>(a, evc, s_bal, lane, limit);
         if (d.depth > dep0) {                     // entered a new node
             entry[dep0 * C_LANES] = (uint32_t)d.nodes;
-            const bool big = (uint32_t)__builtin_popcountll((uint64_t)d.rem) > min_rem;
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             uint32_t cnt = 0;
-            if (big && k.ok && memo_lookup<MODEL, G>(tab, k, h, cnt)) {
-                ++ms.hits;
+            if (k.ok && memo_lookup<MODEL, G>(tab, k, h, cnt)) {
                 if (d.nodes + cnt > limit) {      // the budget falls inside that subtree
                     d.nodes = limit;
                     status = QSMD_STATUS_BUDGET;
@@ -190,7 +179,6 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 3 : 2) void memo_search(Memo
     const int lane = threadIdx.x;
     const uint64_t total = *a.list_count;
     Counters cnt;
-    MemoStats ms{0, 0, 0, 0};
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
     uint32_t* tab = p.table + ((uint64_t)blockIdx.x * C_LANES + (uint64_t)lane) * (uint64_t)p.entries *
@@ -229,7 +217,7 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 3 : 2) void memo_search(Memo
             uint32_t iter = 0;
             do {
                 status = memo_step<MODEL, G, M_LANE>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, tab, h, p.epoch,
-                                                     mask, &s_entry[0][lane], skip, p.min_rem, ms);
+                                                     mask, &s_entry[0][lane], skip);
                 ++iter;
                 if (p.giant_cap && iter >= p.giant_cap && status < 0) {
                     status = QSMD_STATUS_HANDED_OFF;
@@ -242,10 +230,8 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 3 : 2) void memo_search(Memo
                     }
                 }
             } while (status < 0);
-            ms.iters += iter;
-            ms.max_iters = ms.max_iters > iter ? ms.max_iters : iter;
         }
-        if (status == QSMD_STATUS_HANDED_OFF) {  // the split stage searches it (exact, from the root)
+        if (status == QSMD_STATUS_HANDED_OFF) {  // the giant stage searches it (exact, from the root)
             a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
             continue;
         }
@@ -255,16 +241,7 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 3 : 2) void memo_search(Memo
         if (a.witness && status == QSMD_STATUS_LINEARISABLE) dfs.write_witness(a.witness + H.ev_off, H.n_ev);
         cnt.add(status, dfs.nodes);
     }
-    cnt.flush(a.partials, lane);
-    if (p.stats) {                               // diagnostic: iterations, hits, inserts
-        const uint64_t i = wave_sum64(ms.iters), hi = wave_sum64(ms.hits), in = wave_sum64(ms.inserts);
-        if (lane == 0) {
-            atomicAdd(p.stats + 0, (unsigned long long)i);
-            atomicAdd(p.stats + 1, (unsigned long long)hi);
-            atomicAdd(p.stats + 2, (unsigned long long)in);
-        }
-        atomicMax(p.stats + 3, (unsigned long long)ms.max_iters);
-    }
+    cnt.flush(a.buckets, lane);
 }
 
 hipError_t launch_memo(const MemoArgs& p, uint32_t grid, bool wide, hipStream_t s) {

@@ -1,31 +1,37 @@
-// split.hip -- the split stage: one history searched by many lanes
-// (SURVEY.md §8e), and the QSMD_FLAG_MEMO state table.
+// split.hip -- the giant stage: every history the compact and heavy stages
+// hand on (beyond their geometry, or over their work caps), searched by one
+// lane or split over many; then the batch totals.
 //
-// A per-lane search runs as long as its history needs; a wavefront runs as
-// long as its slowest lane.  Heavy-tailed batches (the 10M Bank batch with
-// injected bugs: most histories need tens of nodes, a few need 10^4-10^5)
-// therefore hand every history whose per-lane search reaches the split
-// budget to this stage:
+// One launch per call (giant_search), phases chained inside it by counters:
 //
-//   frontier_search  one lane per giant history.  Runs the reference DFS
-//                    (src/Linearisability.hs:52-69, Lemma L1 state) with a
-//                    cut at depth D: a node reached at depth D (a passed
-//                    postcondition, i.e. a `step` that recurses) is not
-//                    expanded but recorded as a task -- its path and the
-//                    number of nodes the reference has counted up to and
-//                    including it.  D is the smallest depth giving `target`
-//                    tasks (count-only passes, then one emitting pass into a
-//                    contiguous reserved range).
-//   task_search      persistent wavefronts; idle lanes pull tasks with one
-//                    atomic per wavefront.  A lane replays the task's path
-//                    (transitions only, nothing counted), then searches the
-//                    subtree below it (`any' (step ...)`: no children = True).
-//                    A task that decides (True, or Map.! raising) lowers the
-//                    giant's min_win; tasks after it are skipped.
-//   combine_giants   one lane per giant folds the task results in DFS order
-//                    (combine_tasks, internal.h): the reference's count is
-//                    nodes above the cut up to the deciding task + all nodes
-//                    of the subtrees before it + that subtree's count.
+//   frontier  one lane per giant (pulled in chunks of 64).  First the whole
+//             reference DFS (src/Linearisability.hs:52-69, Lemma L1 state)
+//             in the lane, for at most whole_cap iterations (with the exact
+//             memo below when on): most giants end there.  Otherwise the DFS
+//             is cut at depth D: a node reached at depth D (a passed
+//             postcondition, i.e. a `step` that recurses) is not expanded but
+//             recorded as a task -- its path and the number of nodes the
+//             reference has counted up to and including it.  D is the
+//             smallest depth giving `target` tasks (count-only passes, then
+//             one emitting pass into a contiguous reserved range).
+//   tasks     (after every frontier) idle lanes pull tasks with one atomic per
+//             wavefront.  A lane replays the task's path (transitions only,
+//             nothing counted), then searches the subtree below it
+//             (`any' (step ...)`: no children = True).  A task that decides
+//             (True, or Map.! raising) lowers the giant's min_win; tasks
+//             after it are skipped.
+//   combine   (after every task) one lane per giant folds the task results in
+//             DFS order (combine_tasks, internal.h): the reference's count is
+//             nodes above the cut up to the deciding task + all nodes of the
+//             subtrees before it + that subtree's count.
+//   fixup     (QSMD_FLAG_EARLY_EXIT_BATCH, after the combine) histories after
+//             the first failing one become SKIPPED; the totals are recounted.
+//   finish    the last workgroup sums the buckets into the call's totals and
+//             restores the counters for the next call.  With no giant (the
+//             common case) every other workgroup returns at once and
+//             workgroup 0 finishes.
+// A phase waits (polling an agent-scope counter) only on work that running
+// workgroups have already taken, so the chain cannot deadlock.
 //
 // Memo (north star (c)): with QSMD_FLAG_MEMO, a subtree root state (remaining
 // events, model) that was fully searched without success is inserted into an
@@ -39,10 +45,11 @@
 //
 // Generic DFS (GenDFS) over MaskT event bitsets, history in LDS [slot][lane];
 // two variants: <= 64 events / <= 8 pids (u64 masks, 64 lanes) and <= 128
-// events / <= 128 pids (128-bit masks, 16 lanes).
+// events / <= 128 pids (128-bit masks, 16 lanes of the wavefront).
 #include <hip/hip_runtime.h>
 
 #include "internal.h"
+#include "lane.h"
 #include "mask.h"
 #include "models.h"
 
@@ -488,6 +495,8 @@ __device__ __forceinline__ uint32_t variant_of(const qsmd_hdr& H) {
 
 }  // namespace
 
+namespace {
+
 // ---------------------------------------------------------------- frontier
 
 // Search above the cut.  Returns the terminal status; count = tasks reached
@@ -529,125 +538,125 @@ __device__ int top_search(GenDFS<MODEL, MaskT, MAXEV, MAXPID, LANES>& d,
     }
 }
 
-template <uint32_t MODEL, typename MaskT, int MAXEV, int MAXPID, int LANES>
-__global__ __launch_bounds__(LANES) void frontier_search(SplitArgs p, uint32_t variant) {
-    using DFS = GenDFS<MODEL, MaskT, MAXEV, MAXPID, LANES>;
-    __shared__ GLds<MODEL, MaskT, MAXEV, MAXPID, LANES> s;
-    const SearchArgs& a = p.s;
-    const int lane = threadIdx.x;
-    const uint32_t n_g = *p.giant_count;
-    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
-    const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
-    for (uint32_t g = blockIdx.x * LANES + lane; g < n_g; g += gridDim.x * LANES) {
-        const uint32_t h = p.giant_list[g];
-        const qsmd_hdr H = a.hdr[h];
-        if (variant_of(H) != variant) continue;
-        GiantRec G;
-        G.h = h;
-        G.variant = variant;
-        G.first = 0;
-        G.n_tasks = 0;
-        G.depth = 0;
-        G.term_status = QSMD_STATUS_ENCODE_ERROR;
-        G.term_nodes = 0;
-        G.min_win = ~0u;
-        G.pad = 0;
-        DFS d;
-        if (!d.load(a, H, s, lane)) {
-            p.giants[g] = G;
-            continue;
+// The whole search in one lane, for at most `cap` iterations (0 = none):
+// MEMO 0 plain, 1 QSMD_FLAG_MEMO, 2 exact-count memo.  Returns the status,
+// or -1 when the cap was reached first.
+template <int MEMO, uint32_t MODEL, typename MaskT, int MAXEV, int MAXPID, int LANES>
+__device__ int whole_search(GenDFS<MODEL, MaskT, MAXEV, MAXPID, LANES>& d,
+                            GLds<MODEL, MaskT, MAXEV, MAXPID, LANES>& s, const SearchArgs& a, int lane,
+                            uint64_t limit, const Memo& memo, uint32_t g, uint64_t cap, uint64_t t0) {
+    d.init(a, s, lane);
+    uint64_t iter = 0;
+    for (;;) {
+        const int st = d.template step<MEMO>(s, lane, limit, memo, g);
+        if (st >= 0) return st;
+        ++iter;
+        if (cap && iter >= cap) return -1;
+        if (sp_time_up(a, t0, (uint32_t)iter)) {
+            atomicOr(a.timed_out, 1u);
+            return QSMD_STATUS_BUDGET;
         }
-        if (d.n_ev == 0) {
-            G.term_status = QSMD_STATUS_LINEARISABLE;             // :59
-            p.giants[g] = G;
-            continue;
-        }
-        if (p.memo && p.memo_exact) {
-            // first the whole search in this lane with the exact memo, for a
-            // bounded number of iterations: most giants collapse to a few
-            // thousand states (their entries stay for the tasks if not)
-            Memo memo{p.memo, p.memo_mask};
-            memo.epoch = p.memo_epoch;
-            d.init(a, s, lane);
-            int st = -1;
-            uint32_t iter = 0;
-            const uint32_t cap = 64u * p.target;
-            while ((st = d.template step<2>(s, lane, limit, memo, g)) < 0 && ++iter < cap) {
-                if (sp_time_up(a, t0, iter)) {
-                    atomicOr(a.timed_out, 1u);
-                    st = QSMD_STATUS_BUDGET;
-                    break;
-                }
-            }
-            if (st >= 0) {                                         // decided here: no tasks
-                G.term_status = (uint32_t)st;
-                G.term_nodes = d.nodes;
-                if (a.witness && st == QSMD_STATUS_LINEARISABLE) d.path_to(a.witness + H.ev_off, d.n_ev, s, lane);
-                p.giants[g] = G;
-                continue;
-            }
-            // past the cap: the split below (top_search re-initialises the search)
-        }
-        const uint32_t dmax = min(min(p.max_depth, (uint32_t)QSMD_SPLIT_MAX_DEPTH), d.n_ev / 2u);
-        uint32_t cut = 1, count = 0;
-        for (;; ++cut) {
-            top_search(d, s, a, lane, cut, limit, g, 0, nullptr, count, t0);
-            if (count > p.max_tasks && cut > 1) { --cut; break; }
-            if (count >= p.target || cut >= dmax) break;
-        }
-        // reserve a contiguous range; on overflow search the whole history here
-        qsmd_task* region = p.tasks + (uint64_t)variant * p.task_cap;
-        uint32_t first = ~0u;
-        top_search(d, s, a, lane, cut, limit, g, 0, nullptr, count, t0);
-        if (count <= p.max_tasks) {
-            first = atomicAdd(&p.task_count[variant], count);
-            if ((uint64_t)first + count > p.task_cap) {
-                // out of task slots: mark the part of the range below the cap as holes
-                for (uint64_t q = first; q < p.task_cap && q < (uint64_t)first + count; ++q)
-                    region[q].hist = ~0u;
-                first = ~0u;
-            }
-        }
-        int st;
-        if (first != ~0u) {
-            uint32_t emitted = 0;
-            st = top_search(d, s, a, lane, cut, limit, g, count, region + first, emitted, t0);
-            G.first = first;
-            G.n_tasks = count;
-            G.depth = cut;
-        } else {
-            // no task slots left: the whole search here (with the exact memo if on)
-            Memo memo{p.memo, p.memo_mask};
-            memo.epoch = p.memo_epoch;
-            const bool exact = p.memo && p.memo_exact;
-            d.init(a, s, lane);
-            uint32_t iter = 0;
-            while ((st = exact ? d.template step<2>(s, lane, limit, memo, g)
-                               : d.template step<0>(s, lane, limit, memo, 0)) < 0) {
-                if (sp_time_up(a, t0, ++iter)) {
-                    atomicOr(a.timed_out, 1u);
-                    st = QSMD_STATUS_BUDGET;
-                    break;
-                }
-            }
-        }
-        G.term_status = (uint32_t)st;
-        G.term_nodes = d.nodes;
-        if (a.witness && st == QSMD_STATUS_LINEARISABLE) d.path_to(a.witness + H.ev_off, d.n_ev, s, lane);
-        p.giants[g] = G;
     }
+}
+
+// One giant (history p.giant_list[g], of `variant`) in this lane: the whole
+// search first (p.whole_cap iterations; unbounded without a split), then
+// the cut into tasks.  Writes p.giants[g].
+template <uint32_t MODEL, typename MaskT, int MAXEV, int MAXPID, int LANES>
+__device__ void frontier_one(const SplitArgs& p, uint32_t g, uint32_t h, const qsmd_hdr& H, uint32_t variant,
+                             GLds<MODEL, MaskT, MAXEV, MAXPID, LANES>& s, int lane, uint64_t t0) {
+    using DFS = GenDFS<MODEL, MaskT, MAXEV, MAXPID, LANES>;
+    const SearchArgs& a = p.s;
+    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
+    GiantRec G;
+    G.h = h;
+    G.variant = variant;
+    G.first = 0;
+    G.n_tasks = 0;
+    G.depth = 0;
+    G.term_status = QSMD_STATUS_ENCODE_ERROR;
+    G.term_nodes = 0;
+    G.min_win = ~0u;
+    G.pad = 0;
+    DFS d;
+    if (!d.load(a, H, s, lane)) {
+        p.giants[g] = G;
+        return;
+    }
+    if (d.n_ev == 0) {
+        G.term_status = QSMD_STATUS_LINEARISABLE;                 // :59
+        p.giants[g] = G;
+        return;
+    }
+    Memo memo{p.memo, p.memo_mask};
+    memo.epoch = p.memo_epoch;
+    const bool split = p.target != 0;
+    if (!split || p.whole_cap) {
+        // the whole search in this lane (exact memo when on; most giants end here)
+        const uint64_t cap = split ? p.whole_cap : 0;
+        const int st = !p.memo ? whole_search<0>(d, s, a, lane, limit, memo, g, cap, t0)
+                     : p.memo_exact ? whole_search<2>(d, s, a, lane, limit, memo, g, cap, t0)
+                                    : whole_search<1>(d, s, a, lane, limit, memo, g, cap, t0);
+        if (st >= 0) {
+            G.term_status = (uint32_t)st;
+            G.term_nodes = d.nodes;
+            if (a.witness && st == QSMD_STATUS_LINEARISABLE) d.path_to(a.witness + H.ev_off, d.n_ev, s, lane);
+            p.giants[g] = G;
+            return;
+        }
+    }
+    // past the cap: the cut (top_search re-initialises the search)
+    const uint32_t dmax = min(min(p.max_depth, (uint32_t)QSMD_SPLIT_MAX_DEPTH), d.n_ev / 2u);
+    uint32_t cut = 1, count = 0;
+    for (;; ++cut) {
+        top_search(d, s, a, lane, cut, limit, g, 0, nullptr, count, t0);
+        if (count > p.max_tasks && cut > 1) { --cut; break; }
+        if (count >= p.target || cut >= dmax) break;
+    }
+    // reserve a contiguous range; on overflow search the whole history here
+    qsmd_task* region = p.tasks + (uint64_t)variant * p.task_cap;
+    uint32_t first = ~0u;
+    top_search(d, s, a, lane, cut, limit, g, 0, nullptr, count, t0);
+    if (count <= p.max_tasks) {
+        first = atomicAdd(&p.cnt[C_TASKS0 + variant], count);
+        if ((uint64_t)first + count > p.task_cap) {
+            // out of task slots: mark the part of the range below the cap as holes
+            for (uint64_t q = first; q < p.task_cap && q < (uint64_t)first + count; ++q) region[q].hist = ~0u;
+            first = ~0u;
+        }
+    }
+    int st;
+    if (first != ~0u) {
+        uint32_t emitted = 0;
+        st = top_search(d, s, a, lane, cut, limit, g, count, region + first, emitted, t0);
+        G.first = first;
+        G.n_tasks = count;
+        G.depth = cut;
+    } else {
+        // no task slots left: the whole search here
+        st = !p.memo ? whole_search<0>(d, s, a, lane, limit, memo, g, 0, t0)
+           : p.memo_exact ? whole_search<2>(d, s, a, lane, limit, memo, g, 0, t0)
+                          : whole_search<1>(d, s, a, lane, limit, memo, g, 0, t0);
+    }
+    G.term_status = (uint32_t)st;
+    G.term_nodes = d.nodes;
+    if (a.witness && st == QSMD_STATUS_LINEARISABLE) d.path_to(a.witness + H.ev_off, d.n_ev, s, lane);
+    p.giants[g] = G;
 }
 
 // ------------------------------------------------------------------- tasks
 
+// Persistent task search of one variant by the LANES lanes of this
+// wavefront that call it; returns the tasks this wavefront took (holes and
+// skipped ones included).
 template <uint32_t MODEL, typename MaskT, int MAXEV, int MAXPID, int LANES>
-__global__ __launch_bounds__(LANES) void task_search(SplitArgs p, uint32_t variant) {
+__device__ uint32_t task_loop(const SplitArgs& p, uint32_t variant, GLds<MODEL, MaskT, MAXEV, MAXPID, LANES>& s,
+                              int lane, uint64_t t0, uint32_t* head) {
     using DFS = GenDFS<MODEL, MaskT, MAXEV, MAXPID, LANES>;
     constexpr uint32_t kRefillMin = LANES >= 64 ? 8u : 2u;
-    __shared__ GLds<MODEL, MaskT, MAXEV, MAXPID, LANES> s;
     const SearchArgs& a = p.s;
-    const int lane = threadIdx.x;
-    const uint32_t count = min(*(volatile uint32_t*)&p.task_count[variant], p.task_cap);
+    const uint32_t count = min(__hip_atomic_load(&p.cnt[C_TASKS0 + variant], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT), p.task_cap);
     const qsmd_task* tasks = p.tasks + (uint64_t)variant * p.task_cap;
     uint8_t* t_status = p.task_status + (uint64_t)variant * p.task_cap;
     uint64_t* t_nodes = p.task_nodes + (uint64_t)variant * p.task_cap;
@@ -657,10 +666,9 @@ __global__ __launch_bounds__(LANES) void task_search(SplitArgs p, uint32_t varia
     const bool use_memo = p.memo != nullptr;
     const bool exact = use_memo && p.memo_exact;
     const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
-    const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
 
     bool busy = false, exhausted = count == 0;
-    uint32_t idx = 0, g = 0, local = 0, h = 0, iter = 0;
+    uint32_t idx = 0, g = 0, local = 0, h = 0, iter = 0, taken = 0;
     DFS d;
     d.depth = 0;
     d.nodes = 0;
@@ -672,9 +680,10 @@ __global__ __launch_bounds__(LANES) void task_search(SplitArgs p, uint32_t varia
             const int leader = __builtin_ctzll(idle);
             const uint32_t want = (uint32_t)__builtin_popcountll(idle);
             uint32_t first = 0;
-            if (lane == leader) first = atomicAdd(&p.queue_head[variant], want);
+            if (lane == leader) first = atomicAdd(head, want);
             first = __shfl(first, leader, LANES);
             if (first + want >= count) exhausted = true;
+            taken += first >= count ? 0u : min(want, count - first);
             if (!busy) {
                 idx = first + sp_lane_prefix(idle);
                 if (idx < count && tasks[idx].hist != ~0u) {   // ~0u: a hole (frontier overflow)
@@ -731,86 +740,296 @@ __global__ __launch_bounds__(LANES) void task_search(SplitArgs p, uint32_t varia
             }
         }
     }
+    return taken;
 }
 
 // ----------------------------------------------------------------- combine
 
-__global__ __launch_bounds__(64) void combine_giants(SplitArgs p) {
+// Fold giant g's tasks into its history's outputs; returns the status.
+__device__ int combine_one(const SplitArgs& p, uint32_t g, uint64_t& nodes) {
     const SearchArgs& a = p.s;
-    const uint32_t n_g = *p.giant_count;
-    uint64_t c[T_N] = {};
-    for (uint32_t g = blockIdx.x * 64 + threadIdx.x; g < n_g; g += gridDim.x * 64) {
-        const GiantRec G = p.giants[g];
-        const uint32_t h = G.h;
-        const uint64_t base = (uint64_t)G.variant * p.task_cap + G.first;
-        uint64_t nodes = 0;
-        int64_t win = -1;
-        const int st = combine_tasks(G.term_status, G.term_nodes, p.tasks + base, p.task_status + base,
-                                     p.task_nodes + base, G.n_tasks, a.max_nodes, &nodes, &win);
-        note_failure(a, h, st);
-        a.status[h] = (uint8_t)st;
-        if (a.nodes) a.nodes[h] = nodes;
-        if (a.witness && win >= 0 && st == QSMD_STATUS_LINEARISABLE) {
-            const uint8_t* row = p.task_witness + (base + (uint64_t)win) * kTaskWitness;
-            const qsmd_hdr H = a.hdr[h];
-            for (uint32_t q = 0; q < H.n_ev && q < kTaskWitness; ++q) {
-                a.witness[H.ev_off + q] = row[q];
-                if (row[q] == QSMD_WITNESS_END) break;
+    const GiantRec G = p.giants[g];
+    const uint32_t h = G.h;
+    const uint64_t base = (uint64_t)G.variant * p.task_cap + G.first;
+    nodes = 0;
+    int64_t win = -1;
+    const int st = combine_tasks(G.term_status, G.term_nodes, p.tasks + base, p.task_status + base,
+                                 p.task_nodes + base, G.n_tasks, a.max_nodes, &nodes, &win);
+    note_failure(a, h, st);
+    a.status[h] = (uint8_t)st;
+    if (a.nodes) a.nodes[h] = nodes;
+    if (a.witness && win >= 0 && st == QSMD_STATUS_LINEARISABLE) {
+        const uint8_t* row = p.task_witness + (base + (uint64_t)win) * kTaskWitness;
+        const qsmd_hdr H = a.hdr[h];
+        for (uint32_t q = 0; q < H.n_ev && q < kTaskWitness; ++q) {
+            a.witness[H.ev_off + q] = row[q];
+            if (row[q] == QSMD_WITNESS_END) break;
+        }
+    }
+    return st;
+}
+
+// ------------------------------------------------------- phase hand-offs
+
+// After this workgroup's stores: add v to a phase counter (release).
+__device__ __forceinline__ void publish_add(uint32_t* ctr, uint32_t v, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (lane == 0 && v) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(ctr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// A poll of a counter other workgroups update: a global (not flat) sc1
+// load, which bypasses this CU's L1 (a flat load may be served by a stale
+// L1 line, e.g. the counters' line read at kernel start, and spin forever).
+__device__ __forceinline__ uint32_t poll_u32(const uint32_t* c) {
+    using gptr = const __attribute__((address_space(1))) uint32_t*;
+    return __hip_atomic_load((gptr)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait until a phase counter reaches target (acquire).  A safety net bounds
+// the wait by twice the call's time limit (a stuck phase then reports
+// through timed_out instead of holding the GPU).
+__device__ __forceinline__ void wait_for(const uint32_t* ctr, uint32_t target, const SearchArgs& a, uint64_t t0) {
+    uint32_t polls = 0;
+    while (poll_u32(ctr) < target) {
+        __builtin_amdgcn_s_sleep(8);
+        if ((++polls & 63u) == 0u) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (and the L1 refreshed now and then)
+            if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > 2 * a.time_limit) {
+                atomicOr(a.timed_out, 2u);
+                break;
             }
         }
-        if (st == QSMD_STATUS_SKIPPED) continue;
-        c[T_LIN] += st == QSMD_STATUS_LINEARISABLE;
-        c[T_NONLIN] += st == QSMD_STATUS_NONLINEARISABLE;
-        c[T_ERR] += st == QSMD_STATUS_MODEL_ERROR;
-        c[T_ENC] += st == QSMD_STATUS_ENCODE_ERROR;
-        c[T_BUDGET] += st == QSMD_STATUS_BUDGET;
-        c[T_NODES] += nodes;
     }
-    c[T_CHECKED] = c[T_LIN] + c[T_NONLIN] + c[T_ERR];
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t ld_cnt(const uint32_t* c) { return poll_u32(c); }
+
+// The call's last act: totals from the buckets, the probe snapshot for the
+// host, every counter and bucket restored for the next call.
+__device__ void finish_call(const SplitArgs& p, int lane) {
+    unsigned long long* bk = p.s.buckets;
+    unsigned long long* xb = bk + (size_t)kBuckets * kBucketWords;   // early-exit recount
+    const unsigned long long* src = p.early ? xb : bk;
+    uint64_t v[T_N];
 #pragma unroll
-    for (int k = 0; k < T_N; ++k) {
-        uint64_t v = c[k];
+    for (int k = 0; k < T_N; ++k) v[k] = lane < (int)kBuckets ? src[(uint64_t)lane * kBucketWords + k] : 0ull;
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (threadIdx.x == 0) a.partials[(uint64_t)blockIdx.x * T_N + k] = v;
+    for (int k = 0; k < T_N; ++k) v[k] = wave_sum64(v[k]);
+    if (p.totals && lane < T_N) {
+        uint64_t t = 0;
+#pragma unroll
+        for (int k = 0; k < T_N; ++k) t = lane == k ? v[k] : t;
+        reinterpret_cast<unsigned long long*>(p.totals)[lane] = t;
     }
+    if (p.probe_host && lane < 4) p.probe_host[lane] = p.cnt[lane];
+    // restore: buckets (and the early-exit ones), then the counters
+    for (uint32_t i = (uint32_t)lane; i < kBuckets * kBucketWords; i += 64u) {
+        bk[i] = 0ull;
+        if (p.early) xb[i] = 0ull;
+    }
+    if (lane < (int)C_N) p.cnt[lane] = lane == (int)C_FIRST_FAIL ? 0xFFFFFFFFu : 0u;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ kernels
+
+namespace {
+template <uint32_t MODEL>
+struct GiantLds {
+    union {
+        GLds<MODEL, uint64_t, 64, 8, 64> v0;
+        GLds<MODEL, M128, 128, 128, 16> v1;
+    };
+};
+}  // namespace
+
+__device__ __forceinline__ void beat(const SplitArgs& p, int lane, uint32_t k, uint32_t v) {
+    if (p.debug && lane == 0)
+        __hip_atomic_store(p.debug + (uint64_t)blockIdx.x * 4 + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <uint32_t MODEL>
+__global__ __launch_bounds__(64) void giant_search(SplitArgs p) {
+    __shared__ GiantLds<MODEL> u;
+    const SearchArgs& a = p.s;
+    const int lane = threadIdx.x;
+    uint32_t* cnt = p.cnt;
+    const uint32_t n_g = ld_cnt(cnt + C_GIANT);
+    if (n_g == 0 && !p.early) {                 // nothing to do but the totals
+        if (blockIdx.x == 0) finish_call(p, lane);
+        return;
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    beat(p, lane, 0, 1);
+    // ---- frontier: chunks of 64 giants; variant 0 on all lanes, then variant
+    // 1 in four rounds of 16 lanes
+    for (;;) {
+        uint32_t c0 = 0;
+        if (lane == 0) c0 = atomicAdd(cnt + C_GNEXT, 64u);
+        c0 = __shfl(c0, 0, 64);
+        if (c0 >= n_g) break;
+        const uint32_t g = c0 + (uint32_t)lane;
+        const bool in = g < n_g;
+        uint32_t h = 0;
+        qsmd_hdr H{0, 0, 0, 0, 0, 0};
+        if (in) {
+            h = p.giant_list[g];
+            H = a.hdr[h];
+        }
+        const uint32_t var = variant_of(H);
+        if (in && var == 0u) frontier_one<MODEL, uint64_t, 64, 8, 64>(p, g, h, H, 0u, u.v0, lane, t0);
+        __syncthreads();
+        for (uint32_t r = 0; r < 4u; ++r) {
+            if (in && var == 1u && (uint32_t)lane / 16u == r)
+                frontier_one<MODEL, M128, 128, 128, 16>(p, g, h, H, 1u, u.v1, lane & 15, t0);
+            __syncthreads();
+        }
+        publish_add(cnt + C_GDONE, min(64u, n_g - c0), lane);
+        beat(p, lane, 1, c0 + 1);
+    }
+    beat(p, lane, 0, 2);
+    // ---- tasks (every frontier done: the task lists are complete)
+    wait_for(cnt + C_GDONE, n_g, a, t0);
+    beat(p, lane, 0, 3);
+    uint32_t took = task_loop<MODEL, uint64_t, 64, 8, 64>(p, 0u, u.v0, lane, t0, cnt + C_TQ0);
+    __syncthreads();
+    if (lane < 16) {
+        const uint32_t t1 = task_loop<MODEL, M128, 128, 128, 16>(p, 1u, u.v1, lane, t0, cnt + C_TQ1);
+        took += lane == 0 ? t1 : 0u;
+    }
+    took = __shfl(took, 0, 64);
+    publish_add(cnt + C_TDONE, took, lane);
+    beat(p, lane, 0, 4);
+    beat(p, lane, 2, took);
+    // ---- combine (every task done)
+    const uint32_t n_tasks = min(ld_cnt(cnt + C_TASKS0), p.task_cap) + min(ld_cnt(cnt + C_TASKS1), p.task_cap);
+    wait_for(cnt + C_TDONE, n_tasks, a, t0);
+    beat(p, lane, 0, 5);
+    Counters cc;
+    for (;;) {
+        uint32_t c0 = 0;
+        if (lane == 0) c0 = atomicAdd(cnt + C_CNEXT, 64u);
+        c0 = __shfl(c0, 0, 64);
+        if (c0 >= n_g) break;
+        const uint32_t g = c0 + (uint32_t)lane;
+        if (g < n_g) {
+            uint64_t nodes = 0;
+            const int st = combine_one(p, g, nodes);
+            cc.add(st, nodes);
+        }
+        publish_add(cnt + C_CDONE, min(64u, n_g - c0), lane);
+    }
+    cc.flush(a.buckets, lane);
+    // ---- early exit: every history after the first failing one is SKIPPED,
+    // and the totals are recounted from the final outputs
+    if (p.early) {
+        wait_for(cnt + C_CDONE, n_g, a, t0);
+        const uint32_t ff = ld_cnt(a.first_fail);
+        Counters xc;
+        uint64_t skipped = 0;
+        constexpr uint32_t kChunk = 4096;
+        for (;;) {
+            uint32_t c0 = 0;
+            if (lane == 0) c0 = atomicAdd(cnt + C_XNEXT, 1u);
+            const uint64_t b0 = (uint64_t)__shfl(c0, 0, 64) * kChunk;
+            if (b0 >= a.n_hist) break;
+            for (uint64_t hh = b0 + (uint64_t)lane; hh < a.n_hist && hh < b0 + kChunk; hh += 64) {
+                if (hh > ff) {
+                    a.status[hh] = QSMD_STATUS_SKIPPED;
+                    if (a.nodes) a.nodes[hh] = 0;
+                    ++skipped;
+                } else {
+                    xc.add(a.status[hh], a.nodes ? a.nodes[hh] : 0ull);
+                }
+            }
+        }
+        xc.flush(a.buckets + (size_t)kBuckets * kBucketWords, lane);
+        const uint64_t sk = wave_sum64(skipped);
+        bucket_add(a.buckets + (size_t)kBuckets * kBucketWords, blockIdx.x, T_SKIPPED, lane == 0 ? sk : 0ull);
+    }
+    beat(p, lane, 0, 6);
+    // ---- the last workgroup out finishes the call
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint32_t last = 0;
+    if (lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = atomicAdd(cnt + C_EXIT, 1u) == gridDim.x - 1u;
+    }
+    if (__shfl(last, 0, 64)) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        finish_call(p, lane);
+    }
+}
+
+// qsmd_split_frontier: one giant (giant_list[0]), one lane.
+template <uint32_t MODEL, typename MaskT, int MAXEV, int MAXPID, int LANES>
+__global__ __launch_bounds__(LANES) void frontier_kernel(SplitArgs p, uint32_t variant) {
+    __shared__ GLds<MODEL, MaskT, MAXEV, MAXPID, LANES> s;
+    const int lane = threadIdx.x;
+    const uint64_t t0 = p.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (lane == 0) {
+        const uint32_t h = p.giant_list[0];
+        const qsmd_hdr H = p.s.hdr[h];
+        frontier_one<MODEL, MaskT, MAXEV, MAXPID, LANES>(p, 0u, h, H, variant, s, lane, t0);
+    }
+}
+
+// qsmd_check_tasks: the task phase alone over the caller's tasks.
+template <uint32_t MODEL, typename MaskT, int MAXEV, int MAXPID, int LANES>
+__global__ __launch_bounds__(LANES) void task_kernel(SplitArgs p, uint32_t variant) {
+    __shared__ GLds<MODEL, MaskT, MAXEV, MAXPID, LANES> s;
+    const uint64_t t0 = p.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
+    task_loop<MODEL, MaskT, MAXEV, MAXPID, LANES>(p, variant, s, threadIdx.x, t0, p.cnt + C_TQ0 + variant);
 }
 
 // ------------------------------------------------------------------ launch
 
 namespace {
 template <uint32_t MODEL>
-hipError_t launch_split_model(bool frontier, int variant, const SplitArgs& p, uint32_t grid, hipStream_t s) {
+hipError_t launch_parts(bool frontier, int variant, const SplitArgs& p, uint32_t grid, hipStream_t s) {
     if (variant == 0) {
         if (frontier)
-            hipLaunchKernelGGL((frontier_search<MODEL, uint64_t, 64, 8, 64>), dim3(grid), dim3(64), 0, s, p, 0u);
+            hipLaunchKernelGGL((frontier_kernel<MODEL, uint64_t, 64, 8, 64>), dim3(1), dim3(64), 0, s, p, 0u);
         else
-            hipLaunchKernelGGL((task_search<MODEL, uint64_t, 64, 8, 64>), dim3(grid), dim3(64), 0, s, p, 0u);
+            hipLaunchKernelGGL((task_kernel<MODEL, uint64_t, 64, 8, 64>), dim3(grid), dim3(64), 0, s, p, 0u);
     } else {
         if (frontier)
-            hipLaunchKernelGGL((frontier_search<MODEL, M128, 128, 128, 16>), dim3(grid), dim3(16), 0, s, p, 1u);
+            hipLaunchKernelGGL((frontier_kernel<MODEL, M128, 128, 128, 16>), dim3(1), dim3(16), 0, s, p, 1u);
         else
-            hipLaunchKernelGGL((task_search<MODEL, M128, 128, 128, 16>), dim3(grid), dim3(16), 0, s, p, 1u);
+            hipLaunchKernelGGL((task_kernel<MODEL, M128, 128, 128, 16>), dim3(grid), dim3(16), 0, s, p, 1u);
     }
     return hipGetLastError();
 }
 }  // namespace
 
-uint32_t split_lanes(int variant) { return variant == 0 ? 64u : 16u; }
-
-hipError_t launch_frontier(int variant, const SplitArgs& p, uint32_t grid, hipStream_t s) {
-    if (p.s.model_id == QSMD_MODEL_BANK) return launch_split_model<QSMD_MODEL_BANK>(true, variant, p, grid, s);
-    return launch_split_model<QSMD_MODEL_TICKET>(true, variant, p, grid, s);
-}
-
-hipError_t launch_tasks(int variant, const SplitArgs& p, uint32_t grid, hipStream_t s) {
-    if (p.s.model_id == QSMD_MODEL_BANK) return launch_split_model<QSMD_MODEL_BANK>(false, variant, p, grid, s);
-    return launch_split_model<QSMD_MODEL_TICKET>(false, variant, p, grid, s);
-}
-
-hipError_t launch_combine(const SplitArgs& p, uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL(combine_giants, dim3(grid), dim3(64), 0, s, p);
+hipError_t launch_giants(const SplitArgs& p, uint32_t grid, hipStream_t s) {
+    if (p.s.model_id == QSMD_MODEL_BANK)
+        hipLaunchKernelGGL(giant_search<QSMD_MODEL_BANK>, dim3(grid), dim3(64), 0, s, p);
+    else
+        hipLaunchKernelGGL(giant_search<QSMD_MODEL_TICKET>, dim3(grid), dim3(64), 0, s, p);
     return hipGetLastError();
+}
+
+hipError_t launch_frontier_only(int variant, const SplitArgs& p, hipStream_t s) {
+    if (p.s.model_id == QSMD_MODEL_BANK) return launch_parts<QSMD_MODEL_BANK>(true, variant, p, 1, s);
+    return launch_parts<QSMD_MODEL_TICKET>(true, variant, p, 1, s);
+}
+
+hipError_t launch_tasks_only(int variant, const SplitArgs& p, uint32_t grid, hipStream_t s) {
+    if (p.s.model_id == QSMD_MODEL_BANK) return launch_parts<QSMD_MODEL_BANK>(false, variant, p, grid, s);
+    return launch_parts<QSMD_MODEL_TICKET>(false, variant, p, grid, s);
 }
 
 }  // namespace qsmd

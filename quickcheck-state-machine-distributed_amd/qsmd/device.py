@@ -62,8 +62,7 @@ EXPORTS = {
     "qsmd_set_time_limit_ms": (_I, [_P, _U64]),
     "qsmd_set_stage0_grid": (_I, [_P, _U64]),
     "qsmd_set_stage0_budget": (_I, [_P, _U64]),
-    "qsmd_diag_stamps": (_I, [_P, _P]),
-    "qsmd_spread_stats": (_I, [_P, _P]),
+    "qsmd_probe_read": (_I, [_P, _P]),
     "qsmd_wellformed_batch": (_I, [_P, _P, _U64, _P, _U64, _P, _U32, _P]),
     "qsmd_wellformed_batch_device": (_I, [_P, _P, _U64, _P, _U64, _P, _U32, _P, _P]),
     "qsmd_gen_batch_device": (_I, [_P, _P, _U64, _U64, _U32, _P, _P, _P, _P]),   # include/qsmd_gen.h
@@ -293,15 +292,13 @@ class Context:
                                              events_ptr, bug_ptr, stream)
         self._check(rc, "qsmd_gen_batch_device")
 
-    def spread_stats(self):
-        """Spread stage of the last call: (histories, tasks, explored nodes,
-        sum of their reference node counts)."""
-        out = (ctypes.c_uint64 * 4)()
-        self._check(self._lib.qsmd_spread_stats(self._h, out), "qsmd_spread_stats")
-        return tuple(int(x) for x in out)
-
-    def diag_stamps(self, ptr):
-        self._check(self._lib.qsmd_diag_stamps(self._h, ptr), "qsmd_diag_stamps")
+    def probe(self):
+        """Routing of the most recent check call (qsmd_probe_read): histories
+        stage 0 passed to stage 0w, heavy histories of stages 0 and 0w,
+        giants."""
+        out = (ctypes.c_uint32 * 4)()
+        self._check(self._lib.qsmd_probe_read(self._h, out), "qsmd_probe_read")
+        return dict(zip(("deferred", "heavy32", "heavy64", "giants"), (int(x) for x in out)))
 
     def timing_reset(self):
         self._check(self._lib.qsmd_timing_reset(self._h), "qsmd_timing_reset")

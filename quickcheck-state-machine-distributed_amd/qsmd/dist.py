@@ -47,15 +47,27 @@ def allreduce_totals(local_totals, stop_flag=0, group=None):
     import torch.distributed as dist
 
     if isinstance(local_totals, torch.Tensor):
-        t = local_totals
+        t = local_totals.to(torch.int64)
     else:
         t = torch.as_tensor(np.asarray(local_totals, dtype=np.int64))
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        t = t.to(_collective_device(group))            # RCCL: device tensors only
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
         f = torch.tensor([int(stop_flag)], dtype=torch.int64, device=t.device)
         dist.all_reduce(f, op=dist.ReduceOp.MAX, group=group)
         stop_flag = int(f.item())
     return t.cpu().numpy().astype(np.int64), int(stop_flag)
+
+
+def _collective_device(group=None):
+    """Where a collective's tensors must live: the current GPU under the nccl
+    backend (RCCL over xGMI takes device tensors only), the host under gloo."""
+    import torch
+    import torch.distributed as dist
+
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
 
 
 def check_sharded(checker, gen_params, n_total, rank, world, group=None):
@@ -93,8 +105,7 @@ def _allreduce(arr, op, group=None):
 
     t = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.int64))
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        if dist.get_backend(group) == "nccl":          # RCCL: device tensors
-            t = t.to(torch.device("cuda", torch.cuda.current_device()))
+        t = t.to(_collective_device(group))
         dist.all_reduce(t, op=op, group=group)
     return t.cpu().numpy().astype(np.int64)
 

@@ -81,29 +81,38 @@ def test_random_any_shape(ctx, model):
     _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
 
 
+DEFAULTS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 2, "wave_budget": 16, "wave_max": 16384,
+            "split_budget": 1024, "memo_lane_entries": 256, "memo_grid": 2048, "split_xmemo": 1}
+
+
+@pytest.fixture
+def knobs(ctx):
+    """Set tuning knobs for one test; every knob is restored afterwards."""
+    def set_(**kw):
+        for k, v in kw.items():
+            ctx.set_param(k, v)
+    yield set_
+    for k, v in DEFAULTS.items():
+        ctx.set_param(k, v)
+
+
 @pytest.mark.parametrize("n_ev,n_pid", [(40, 3), (64, 6), (96, 4), (128, 8), (60, 20), (128, 100)])
-@pytest.mark.parametrize("stage0w", ["on", "off", "coop", "memo", "no_heavy"])
-def test_stage_cascade(ctx, n_ev, n_pid, stage0w):
+@pytest.mark.parametrize("w_budget,heavy", [(32, 0), (4, 0), (4, 1), (0, 0)])
+def test_stage_cascade(ctx, knobs, n_ev, n_pid, w_budget, heavy):
     """Histories beyond stage 0 (32 events / 8 pids) go through stage 0w
-    (<= 64 events, <= 8 pids; over its node budget: coop64; off: straight to
-    stage 1) and stages 1 and 2.  coop: a 4-node budget sends most of them to
-    coop64; no_heavy (the default): stage 0w searches them to the end."""
+    (<= 64 events, <= 8 pids; over its node budget: the heavy stage, one
+    wavefront or one lane per history) and the giant stage (everything
+    else).  A 4-node budget sends most 0w histories to the heavy stage; 0
+    = stage 0w searches them to the end."""
     rng = random.Random(n_ev * 1000 + n_pid)
-    ctx.set_param("stage0w", 0 if stage0w == "off" else 1)
-    ctx.set_param("stage0w_budget", {"coop": 4, "memo": 4, "on": 32}.get(stage0w, 0))
-    ctx.set_param("memo_stage", 0 if stage0w == "coop" else 1)
-    try:
-        for model in ("ticket", "bank"):
-            hs = [histgen.wellformed_history(rng, model, n_ev // 2, n_pid, p_pending=0.0)[:n_ev]
-                  for _ in range(300)]
-            hs += [histgen.random_history(rng, model, n_ev, n_pid) for _ in range(300)]
-            m = models.BY_NAME[model]
-            b = codec.encode(m, hs)
-            _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
-    finally:
-        ctx.set_param("stage0w", 1)
-        ctx.set_param("stage0w_budget", 32)
-        ctx.set_param("memo_stage", 1)
+    knobs(stage0w_budget=w_budget, heavy_mode=heavy)
+    for model in ("ticket", "bank"):
+        hs = [histgen.wellformed_history(rng, model, n_ev // 2, n_pid, p_pending=0.0)[:n_ev]
+              for _ in range(300)]
+        hs += [histgen.random_history(rng, model, n_ev, n_pid) for _ in range(300)]
+        m = models.BY_NAME[model]
+        b = codec.encode(m, hs)
+        _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
 
 
 @pytest.mark.parametrize("model,n_ev", [("bank", 32), ("bank", 20), ("ticket", 24), ("ticket", 7),
@@ -111,7 +120,8 @@ def test_stage_cascade(ctx, n_ev, n_pid, stage0w):
 def test_packed_uniform_batches(ctx, model, n_ev):
     """Batches whose histories are packed back to back with one length take the
     coalesced staging path; corrupt some events (encode errors) and widen some
-    values (deferral to stage 1) so every outcome goes through that path."""
+    values (deferral beyond the compact stages) so every outcome goes through
+    that path."""
     rng = random.Random(n_ev * 7 + len(model))
     m = models.BY_NAME[model]
     hs = []
@@ -141,136 +151,76 @@ def test_mixed_sizes_one_batch(ctx):
 
 @pytest.mark.parametrize("name,n", [("ticket_2x10", 20000), ("bank_4x16", 50000),
                                     ("bank_4x16_bugs", 50000), ("bank_6x24", 20000)])
-@pytest.mark.parametrize("budget", [0, 24])
-@pytest.mark.parametrize("kernel", [0, 1, 2])
-def test_generated_configs(ctx, name, n, budget, kernel):
-    """kernel 0: compact_search (2: with groups from a counter on a
-    persistent grid); budget > 0: histories over the stage-0 node budget go
-    to the heavy stages.  kernel 1: group_search (in-wave sharing; the budget
-    does not apply)."""
-    if kernel == 1 and budget:
-        pytest.skip("group_search has no stage-0 budget")
-    ctx.set_param("stage0_kernel", 1 if kernel == 1 else 0)
-    ctx.set_param("stage0_dynamic", 1 if kernel == 2 else 0)
-    if kernel == 2:
-        ctx.set_param("stage0_grid", 97)
-    ctx.set_stage0_budget(budget)
-    try:
-        hdr, ev, bug = gen.generate_config(name, 0, n)
-        st, nd, _ = _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
-    finally:
-        ctx.set_stage0_budget(0)
-        ctx.set_param("stage0_auto", 1)
-        ctx.set_param("stage0_kernel", 0)
-        ctx.set_param("stage0_dynamic", 0)
-        ctx.set_param("stage0_grid", 65536)
+@pytest.mark.parametrize("budget", [0, 8, 32])
+@pytest.mark.parametrize("heavy", [0, 1])
+def test_generated_configs(ctx, knobs, name, n, budget, heavy):
+    """The generated BASELINE configurations through the cascade: stage-0
+    budget 0 (stage 0 searches everything), 8 (most histories go to the
+    heavy stage) and 32 (the default); heavy stage in wave mode (one
+    wavefront per history, LDS memo) and lane mode (one lane per history,
+    HBM memo)."""
+    knobs(stage0_budget=budget, stage0w_budget=budget, heavy_mode=heavy)
+    hdr, ev, bug = gen.generate_config(name, 0, n)
+    st, nd, _ = _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
     if name in ("bank_4x16", "bank_6x24"):
         assert (st == codec.STATUS_LIN).all()
 
 
-@pytest.mark.parametrize("name,n", [("ticket_2x10", 20000), ("bank_4x16", 50000), ("bank_4x16_bugs", 50000)])
-@pytest.mark.parametrize("rerun,budget", [(16, 0), (3, 0), (16, 256), (5, 40)])
-def test_rerun_stage(ctx, name, n, rerun, budget):
-    """Stage 0r: stage 0 stops at `rerun` nodes and the histories over it are
-    searched again from the root (packed, list mode), with the stage-0 heavy
-    budget (and the caller's max_nodes: budget 40 < the heavy budget)."""
-    ctx.set_param("rerun_budget", rerun)
-    ctx.set_stage0_budget(budget)
-    try:
-        hdr, ev, _ = gen.generate_config(name, 3, n)
-        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=40 if rerun == 5 else 10**7)
-    finally:
-        ctx.set_param("rerun_budget", 0)
-        ctx.set_stage0_budget(0)
-        ctx.set_param("stage0_auto", 1)
-
-
-MEMO_CASES = [("bank_4x16_bugs", 50000, 64, 0), ("bank_4x16_bugs", 20000, 8, 300), ("bank_4x16", 50000, 16, 0),
+LANE_CASES = [("bank_4x16_bugs", 50000, 64, 0), ("bank_4x16_bugs", 20000, 8, 300), ("bank_4x16", 50000, 16, 0),
               ("ticket_2x10", 20000, 4, 0), ("bank_6x24", 20000, 16, 0), ("bank_6x24", 20000, 8, 500)]
 
 
-@pytest.mark.parametrize("name,n,budget,max_nodes", MEMO_CASES)
+@pytest.mark.parametrize("name,n,budget,max_nodes", LANE_CASES)
 @pytest.mark.parametrize("entries", [128, 2])
-def test_memo_stage(ctx, name, n, budget, max_nodes, entries):
-    """The memo stage (exact-count state memo): histories over the stage-0
-    (stage-0w for 48 events) budget are searched with subtree counts reused
-    from a per-lane table; verdicts, node counts and witnesses must equal the
+def test_lane_mode(ctx, knobs, name, n, budget, max_nodes, entries):
+    """Lane mode of the heavy stage (exact-count state memo in a private HBM
+    table per lane): verdicts, node counts and witnesses must equal the
     reference's.  2 entries: constant replacement; max_nodes: the budget
     falls inside reused subtrees."""
-    ctx.set_param("memo_stage", 1)
-    ctx.set_param("memo_lane_entries", entries)
-    ctx.set_stage0_budget(budget)
-    ctx.set_param("stage0w_budget", budget)
-    try:
-        hdr, ev, _ = gen.generate_config(name, 5, n)
-        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
-    finally:
-        ctx.set_param("memo_lane_entries", 128)
-        ctx.set_stage0_budget(0)
-        ctx.set_param("stage0_auto", 1)
-        ctx.set_param("stage0w_budget", 32)
-        ctx.set_param("stage0_auto", 1)
+    knobs(heavy_mode=1, memo_lane_entries=entries, stage0_budget=budget, stage0w_budget=budget)
+    hdr, ev, _ = gen.generate_config(name, 5, n)
+    _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
 
 
-@pytest.mark.parametrize("name,n", [("bank_4x16", 50000), ("bank_4x16_bugs", 30000), ("ticket_2x10", 20000),
-                                    ("bank_6x24", 20000)])
-@pytest.mark.parametrize("cut_k,cut_min", [(2, 16), (8, 4), (63, 4)])
-def test_straggler_cut(ctx, name, n, cut_k, cut_min):
-    """Straggler cut: once a wavefront has run cut_min iterations with at most
-    cut_k lanes still searching, those histories go to the memo stage and are
-    searched again from the root (63: nearly every history is cut)."""
-    ctx.set_param("cut_k", cut_k)
-    ctx.set_param("cut_min", cut_min)
-    try:
-        hdr, ev, _ = gen.generate_config(name, 13, n)
-        for _ in range(2):                       # the cascade's quiet mode, then its decision
-            _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
-        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=30)
-    finally:
-        ctx.set_param("cut_k", 0)
-        ctx.set_param("cut_min", 16)
+@pytest.mark.parametrize("name,n,budget,max_nodes", LANE_CASES)
+@pytest.mark.parametrize("wave_budget", [1, 4, 16, 64])
+def test_wave_mode(ctx, knobs, name, n, budget, max_nodes, wave_budget):
+    """Wave mode of the heavy stage: one wavefront per history, tasks split
+    to idle lanes after wave_budget nodes (1: a split at nearly every node),
+    the LDS state memo shared by the lanes; max_nodes falls inside reused
+    subtrees and across tasks."""
+    knobs(heavy_mode=0, wave_budget=wave_budget, stage0_budget=budget, stage0w_budget=budget)
+    hdr, ev, _ = gen.generate_config(name, 6, n)
+    _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
 
 
-def test_memo_tables_too_large_fall_back_to_coop_spread(ctx):
-    """Memo tables the device cannot hold switch the context to the coop /
-    spread heavy stages: the same results."""
-    ctx.set_param("memo_grid", 65536)
-    ctx.set_param("memo_lane_entries", 65536)
-    try:
-        hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 21, 20000)
-        for _ in range(2):
-            _compare(ctx, models.MODEL_BANK, hdr, ev)
-    finally:
-        ctx.set_param("memo_grid", 2048)
-        ctx.set_param("memo_lane_entries", 256)
-        ctx.set_param("memo_stage", 1)
+def test_lane_tables_too_large_fall_back_to_wave_mode(ctx, knobs):
+    """Lane-mode tables the device cannot hold keep the context in wave mode:
+    the same results."""
+    knobs(heavy_mode=1, memo_grid=65536, memo_lane_entries=65536, stage0_budget=8)
+    hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 21, 20000)
+    for _ in range(2):
+        _compare(ctx, models.MODEL_BANK, hdr, ev)
 
 
-@pytest.mark.parametrize("split_budget", [16, 200])
-def test_memo_stage_handoff(ctx, split_budget):
-    """Memo-stage searches that reach the giant cap (= split budget
-    iterations) go to the split stage and are searched there from the root;
-    also the default cascade outside heavy mode (stage 0 budget = split
-    budget, then the memo stage)."""
-    ctx.set_param("split_budget", split_budget)
-    try:
-        for name, n in (("bank_4x16_bugs", 30000), ("ticket_2x10", 20000), ("bank_6x24", 5000)):
-            hdr, ev, _ = gen.generate_config(name, 9, n)
-            ctx.set_param("stage0_auto", 0)
-            ctx.set_param("stage0_budget", split_budget)
-            _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
-            ctx.set_param("stage0_auto", 1)
-            for _ in range(2):
-                _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
-    finally:
-        ctx.set_param("split_budget", 1024)
-        ctx.set_param("stage0_auto", 1)
+@pytest.mark.parametrize("split_budget", [1, 16, 200])
+@pytest.mark.parametrize("heavy", [0, 1])
+def test_heavy_handoff_to_giants(ctx, knobs, split_budget, heavy):
+    """Heavy-stage searches past their cap (64 x split budget iterations) go
+    to the giant stage and are searched there again from the root (whole,
+    or cut into tasks after 16 x split budget iterations)."""
+    knobs(split_budget=split_budget, heavy_mode=heavy, stage0_budget=4, stage0w_budget=4)
+    for name, n in (("bank_4x16_bugs", 30000), ("ticket_2x10", 20000), ("bank_6x24", 5000)):
+        hdr, ev, _ = gen.generate_config(name, 9, n)
+        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
 
 
 @pytest.mark.parametrize("model", ["ticket", "bank"])
-def test_memo_stage_any_shape(ctx, model):
-    """Unpaired, shared-pid and pending histories (the general DFS mode) and a
-    non-default model0 through the memo stage."""
+@pytest.mark.parametrize("heavy", [0, 1])
+def test_heavy_any_shape(ctx, knobs, model, heavy):
+    """Unpaired, shared-pid, pending and stray-response histories (the
+    general DFS mode), Map.! errors, node budgets and a non-default model0
+    through the heavy stage."""
     rng = random.Random(77 if model == "ticket" else 78)
     hs = []
     for _ in range(4000):
@@ -279,16 +229,33 @@ def test_memo_stage_any_shape(ctx, model):
         else:
             hs.append(histgen.wellformed_history(rng, model, rng.randint(6, 16), rng.randint(1, 5)))
     m = models.BY_NAME[model]
-    ctx.set_param("memo_stage", 1)
-    ctx.set_stage0_budget(4)
-    try:
-        b = codec.encode(m, hs)
-        _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
-        if model == "ticket":
-            _compare(ctx, m.model_id, b.hdr, b.events, models.TicketModel(1, 0, 3), max_nodes=200000)
-    finally:
-        ctx.set_stage0_budget(0)
-        ctx.set_param("stage0_auto", 1)
+    knobs(heavy_mode=heavy, stage0_budget=4, wave_budget=2)
+    b = codec.encode(m, hs)
+    for max_nodes in (0, 50, 3000):
+        _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=max_nodes)
+    if model == "ticket":
+        _compare(ctx, m.model_id, b.hdr, b.events, models.TicketModel(1, 0, 3), max_nodes=200000)
+
+
+def test_heavy_mode_auto_switches(ctx, knobs):
+    """heavy_mode 2 (the default) picks wave or lane mode from the routing of
+    the last finished call; results are exact whichever it picks and across
+    the switches (bug-heavy batch, a clean one, the bug-heavy again)."""
+    knobs(wave_max=1000)
+    b3 = gen.generate_config("bank_4x16_bugs", 11, 30000)
+    b2 = gen.generate_config("bank_4x16", 11, 30000)
+    for hdr, ev, _ in (b3, b3, b3, b2, b2, b3):
+        _compare(ctx, models.MODEL_BANK, hdr, ev)
+
+
+def test_probe_routing(ctx, knobs):
+    """qsmd_probe_read: how the last call routed its histories."""
+    knobs(stage0_budget=32)
+    hdr, ev, _ = gen.generate_config("bank_4x16", 0, 20000)
+    st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr, ev, threads=8)
+    ctx.check_arrays(models.MODEL_BANK, hdr, ev)
+    pr = ctx.probe()
+    assert pr["heavy32"] == int((nd_o > 32).sum()) and pr["deferred"] == 0 and pr["giants"] == 0
 
 
 def test_concurrent_contexts_on_streams(ctx):
@@ -310,7 +277,7 @@ def test_concurrent_contexts_on_streams(ctx):
                  torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
             bufs.append(b)
         torch.cuda.synchronize()
-        for _ in range(3):                     # the cascade's quiet mode, then its decision
+        for _ in range(3):
             for (hdr, ev, _), c, s, b in zip(batches, ctxs, streams, bufs):
                 c.check_device(models.MODEL_BANK, b[0].data_ptr(), len(hdr), b[1].data_ptr(), len(ev),
                                b[2].data_ptr(), b[3].data_ptr(), None, None, stream=s.cuda_stream)
@@ -322,6 +289,34 @@ def test_concurrent_contexts_on_streams(ctx):
     finally:
         for c in ctxs[1:]:
             c.close()
+
+
+def test_one_context_two_streams(ctx):
+    """Calls of ONE context enqueued back to back on two different streams:
+    the library orders them (they share the context's workspace), so every
+    call's results are the oracle's."""
+    torch = pytest.importorskip("torch")
+    dev = torch.device("cuda:0")
+    batches = [gen.generate_config(name, 41, n) for name, n in (("bank_4x16_bugs", 20000), ("bank_4x16", 40000))]
+    streams = [torch.cuda.Stream(dev) for _ in batches]
+    bufs = []
+    for hdr, ev, _ in batches:
+        n = len(hdr)
+        bufs.append((torch.from_numpy(hdr.view(np.uint8)).to(dev), torch.from_numpy(ev.view(np.uint8)).to(dev),
+                     torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev),
+                     torch.zeros(8, dtype=torch.int64, device=dev)))
+    torch.cuda.synchronize()
+    for _ in range(4):
+        for (hdr, ev, _), s, b in zip(batches, streams, bufs):
+            ctx.check_device(models.MODEL_BANK, b[0].data_ptr(), len(hdr), b[1].data_ptr(), len(ev),
+                             b[2].data_ptr(), b[3].data_ptr(), None, b[4].data_ptr(), stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    for (hdr, ev, _), b in zip(batches, bufs):
+        st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr, ev, None, 0, 8, witness=False)
+        assert np.array_equal(b[2].cpu().numpy(), st_o)
+        assert np.array_equal(b[3].cpu().numpy().astype(np.uint64), nd_o.astype(np.uint64))
+        tot = b[4].cpu().numpy()
+        assert int(tot[7]) == int(nd_o.astype(np.int64).sum()) and int(tot[0]) == len(hdr)
 
 
 def test_model0(ctx):
@@ -340,32 +335,26 @@ def test_model0(ctx):
     del accts
 
 
-def test_budget(ctx):
-    """The caller's max_nodes through every stage: stage-0 budgets 0/5/50
-    (heavy stages), and for 33..64 events stage 0w's budget (32, the default:
-    the memo stage; 4 without the memo stage: coop64 with its exploration cap)."""
+def test_budget(ctx, knobs):
+    """The caller's max_nodes through every stage: stage-0 budgets 0 / 5 / 50
+    (the heavy stage in wave and lane mode), stage-0w budgets 0 / 4 / 256,
+    and the giant stage (a 1-node split budget)."""
     rng = random.Random(5)
     for n_ev in (40, 24):
         hs = [histgen.random_history(rng, "ticket", n_ev, 1) for _ in range(500)]
         b = codec.encode(models.TICKET, hs)
-        for stage0, w_budget, memo in ((0, 0, 1), (5, 0, 1), (50, 0, 0), (0, 4, 0), (0, 4, 1), (0, 256, 1)):
-            ctx.set_stage0_budget(stage0)
-            ctx.set_param("stage0w_budget", w_budget)
-            ctx.set_param("memo_stage", memo)
-            try:
-                for budget in (1, 7, 100, 1000):
-                    st, nd, _ = _compare(ctx, models.MODEL_TICKET, b.hdr, b.events, max_nodes=budget)
-                    assert (nd <= budget).all()
-            finally:
-                ctx.set_stage0_budget(0)
-                ctx.set_param("stage0_auto", 1)
-                ctx.set_param("stage0w_budget", 32)
-                ctx.set_param("memo_stage", 1)
+        for stage0, w_budget, heavy, split in ((0, 0, 0, 1024), (5, 0, 0, 1024), (50, 0, 1, 1024),
+                                               (0, 4, 0, 1024), (0, 4, 1, 1024), (0, 256, 0, 1024),
+                                               (5, 4, 0, 1)):
+            knobs(stage0_budget=stage0, stage0w_budget=w_budget, heavy_mode=heavy, split_budget=split)
+            for budget in (1, 7, 100, 1000):
+                st, nd, _ = _compare(ctx, models.MODEL_TICKET, b.hdr, b.events, max_nodes=budget)
+                assert (nd <= budget).all()
 
 
 @pytest.mark.parametrize("name,shift", [("bank_4x16_bugs", 0), ("bank_4x16_bugs", 3000),
                                         ("bank_6x24", 0), ("bank_4x16", 0)])
-def test_early_exit_batch(ctx, name, shift):
+def test_early_exit_batch(ctx, knobs, name, shift):
     """QSMD_FLAG_EARLY_EXIT_BATCH: like QuickCheck stopping at the first
     failing test, everything after the first non-linearisable (or raising)
     history is SKIPPED; everything up to it is exactly the full result."""
@@ -380,13 +369,9 @@ def test_early_exit_batch(ctx, name, shift):
     st_o, nd_o, _ = oracle_c.check_batch(mid, hdr, ev, threads=8, max_nodes=10**7)
     fails = np.nonzero((st_o == 0) | (st_o == 2))[0]
     cut = int(fails[0]) if len(fails) else len(hdr)
-    ctx.set_stage0_budget(32 if shift else 0)
-    try:
-        st, nd, _, tot = ctx.check_arrays(mid, hdr, ev, flags=device.QSMD_FLAG_EXHAUSTIVE |
-                                          device.QSMD_FLAG_EARLY_EXIT_BATCH, max_nodes=10**7)
-    finally:
-        ctx.set_stage0_budget(0)
-        ctx.set_param("stage0_auto", 1)
+    knobs(stage0_budget=32 if shift else 0)
+    st, nd, _, tot = ctx.check_arrays(mid, hdr, ev, flags=device.QSMD_FLAG_EXHAUSTIVE |
+                                      device.QSMD_FLAG_EARLY_EXIT_BATCH, max_nodes=10**7)
     assert np.array_equal(st[:cut + 1], st_o[:cut + 1]) and np.array_equal(nd[:cut + 1], nd_o[:cut + 1])
     assert (st[cut + 1:] == codec.STATUS_SKIPPED).all() and (nd[cut + 1:] == 0).all()
     assert tot["skipped"] == max(0, len(hdr) - cut - 1)
@@ -413,8 +398,9 @@ def test_encode_errors(ctx):
 
 def test_device_resident_full_size(ctx):
     """BASELINE config 2 at full size (1M histories) through the device entry
-    point; size-independent properties (all linearisable by construction,
-    totals == sums) plus an exact oracle comparison on a sample."""
+    point: size-independent properties (all linearisable by construction,
+    totals == sums) and the oracle's verdict and node count for every
+    history."""
     torch = pytest.importorskip("torch")
     n = 1_000_000
     hdr, ev, bug = gen.generate_config("bank_4x16", 0, n)
@@ -434,9 +420,8 @@ def test_device_resident_full_size(ctx):
     assert (st == codec.STATUS_LIN).all()
     assert int(tot[0]) == n and int(tot[1]) == n and int(tot[7]) == int(nd.sum())
     assert (nd >= 16).all()
-    idx = np.arange(0, n, 50)
-    st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr[idx], ev, threads=8)
-    assert np.array_equal(st_o, st[idx]) and np.array_equal(nd_o, nd[idx])
+    st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr, ev, threads=8)
+    assert np.array_equal(st_o, st) and np.array_equal(nd_o, nd)
 
 
 @pytest.mark.parametrize("packed", [True, False])
@@ -466,84 +451,3 @@ def test_value_ranges_and_pairing(ctx, packed):
     if not packed:
         hdr = hdr[nr.permutation(len(hdr))]
     _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**6)
-
-
-HEAVY_DEFAULTS = {"memo_stage": 0, "stage0_budget": 0, "heavy_stage": 2, "coop_budget": 16, "spread_budget": 128,
-                  "spread_cap": 1 << 22, "coop_max": 4096, "stage0_kernel": 0, "group_budget": 16,
-                  "share_idle": 16, "share_nodes": 32}
-
-
-def _heavy(ctx, **kw):
-    for k, v in {**HEAVY_DEFAULTS, **kw}.items():
-        ctx.set_param(k, v)
-
-
-@pytest.mark.parametrize("name,n", [("bank_4x16_bugs", 20000), ("bank_4x16", 20000), ("ticket_2x10", 20000)])
-@pytest.mark.parametrize("stage,task_budget,cap", [("coop", 1, 0), ("coop", 4, 0), ("coop", 64, 0),
-                                                   ("spread", 4, 1 << 22), ("spread", 128, 1 << 22),
-                                                   ("spread", 8, 1024), ("auto-coop", 16, 0),
-                                                   ("auto-spread", 64, 1 << 22), ("group", 1, 0),
-                                                   ("group", 4, 0), ("group", 16, 0), ("group", 64, 0)])
-def test_heavy_stage(ctx, name, n, stage, task_budget, cap):
-    """The stages for the histories over the stage-0 node budget: coop (one
-    wavefront per history, csrc/coop.hip) and spread (global dynamic split,
-    csrc/spread.hip).  Tiny task budgets force deep split trees; a tiny
-    spread capacity forces its 'no room: search on' path.  Verdicts, node
-    counts and witnesses must be exactly the single DFS's."""
-    hdr, ev, _ = gen.generate_config(name, 3, n)
-    if stage == "coop":
-        _heavy(ctx, stage0_kernel=0, stage0_budget=8, heavy_stage=0, coop_budget=task_budget)
-    elif stage == "spread":
-        _heavy(ctx, stage0_kernel=0, stage0_budget=8, heavy_stage=1, spread_budget=task_budget, spread_cap=cap)
-    elif stage == "group":
-        _heavy(ctx, stage0_kernel=1, group_budget=task_budget, share_idle=1 + task_budget % 7, share_nodes=2)
-    else:                                        # auto: the count decides (1 history -> spread)
-        _heavy(ctx, stage0_kernel=0, stage0_budget=8, heavy_stage=2, coop_budget=task_budget,
-               spread_budget=task_budget, coop_max=1 << 20 if stage == "auto-coop" else 0)
-    try:
-        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev)
-    finally:
-        _heavy(ctx, memo_stage=1)
-
-
-@pytest.mark.parametrize("model", ["ticket", "bank"])
-@pytest.mark.parametrize("stage", ["coop", "spread", "group"])
-def test_heavy_any_shape(ctx, model, stage):
-    """Shared pids, pending invocations, stray responses, Map.! errors and
-    node budgets through the heavy stages (general, unpaired search)."""
-    rng = random.Random(77 if model == "ticket" else 78)
-    hs = []
-    for _ in range(4000):
-        if rng.random() < 0.5:
-            hs.append(histgen.random_history(rng, model, rng.randint(8, 32), rng.randint(1, 3)))
-        else:
-            hs.append(histgen.wellformed_history(rng, model, rng.randint(6, 16), rng.randint(2, 6)))
-    m = models.BY_NAME[model]
-    b = codec.encode(m, hs)
-    if stage == "coop":
-        _heavy(ctx, stage0_kernel=0, stage0_budget=4, heavy_stage=0, coop_budget=2)
-    elif stage == "spread":
-        _heavy(ctx, stage0_kernel=0, stage0_budget=4, heavy_stage=1, spread_budget=6)
-    else:
-        _heavy(ctx, stage0_kernel=1, group_budget=3, share_idle=2, share_nodes=3)
-    try:
-        for max_nodes in (0, 50, 3000):
-            _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=max_nodes)
-    finally:
-        _heavy(ctx, memo_stage=1)
-
-
-def test_adaptive_cascade(ctx):
-    """The default adaptive cascade: a call's probe (histories needing more
-    than 256 nodes) decides whether later calls run stage 0 with a node budget
-    and the heavy stages.  Results are exact in both modes and across the
-    switches (bug-heavy batch, then a clean one, then the bug-heavy again)."""
-    ctx.set_param("stage0_auto", 1)
-    try:
-        b3 = gen.generate_config("bank_4x16_bugs", 11, 30000)
-        b2 = gen.generate_config("bank_4x16", 11, 30000)
-        for hdr, ev, _ in (b3, b3, b3, b2, b2, b3):
-            _compare(ctx, models.MODEL_BANK, hdr, ev)
-    finally:
-        ctx.set_stage0_budget(0)
-        ctx.set_param("stage0_auto", 1)

@@ -37,7 +37,7 @@ def knobs(ctx, split=None, stage0=None):
         yield
     finally:
         ctx.set_split_budget(DEFAULT_SPLIT)
-        ctx.set_param("stage0_auto", 1)
+        ctx.set_stage0_budget(32)
 
 
 @pytest.mark.parametrize("split", [1, 16, 200])
@@ -66,7 +66,7 @@ def test_split_random_shapes(ctx, model):
         _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
 
 
-def test_split_after_refill(ctx):
+def test_split_after_heavy_stage(ctx):
     hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 1000, 20000)
     with knobs(ctx, split=64, stage0=8):
         _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**7)
@@ -238,8 +238,9 @@ def test_adversarial_exhaustive_exact_memo(ctx, nc, no, status, nodes):
 @pytest.mark.parametrize("split", [64, 4096])
 def test_ticket_8x64_batch(ctx, xmemo, split):
     """Batches of 8-client x 64-op TicketDispenser histories (128 events:
-    stage 2, a heavy tail into the split stage), with and without the split
-    stage's exact memo: the reference's verdicts, counts and witnesses."""
+    straight to the giant stage, most decided by its whole search, a heavy
+    tail split into tasks), with and without the giant stage's exact memo:
+    the reference's verdicts, counts and witnesses."""
     hdr, ev, _ = gen.generate_config("ticket_8x64", 0, 1500 if xmemo else 400)
     ctx.set_param("split_xmemo", xmemo)
     try:

@@ -36,7 +36,7 @@ def test_abi_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(device.EXPORTS) == set(names)
-    assert device.load_library().qsmd_abi_version() == 1
+    assert device.load_library().qsmd_abi_version() == 2
 
 
 def test_gen_abi_exports():

@@ -1,0 +1,14 @@
+#!/bin/bash
+# GPU check: smoke, the -m gpu parity suite (stop at the first failure), a
+# short bench.  Every GPU step has its own time limit; the chain stops at the
+# first failing step.
+set -o pipefail
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS} \
+    > gpurun_out/pytest.log 2>&1 &&
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?
+tail -3 gpurun_out/smoke.log; tail -5 gpurun_out/pytest.log; cat gpurun_out/bench.json 2>/dev/null | head -c 1500
+exit $rc
