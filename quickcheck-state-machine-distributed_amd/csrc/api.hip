@@ -57,11 +57,13 @@ struct qsmd_ctx {
     uint64_t split_budget = 1024;      // giant stage: whole-search iterations = 16x, heavy-stage cap = 64x
     uint64_t wave_budget = 16;         // heavy stage: nodes a task searches before it may split
     uint64_t wave_grid = 0;            // heavy stage workgroups (0 = 3 per CU)
+    uint64_t wave_min_rem = 8;         // heavy stage: nodes with at most this many events left skip the memo
+    unsigned long long* wave_stats = nullptr;   // diagnostic (wave_stats_ptr): 8 x u64 per workgroup
     uint64_t giant_grid = 0;           // giant stage workgroups (0 = 2 per CU)
     // heavy stage: one wavefront per history (wave_search) unless the last
     // finished call sent more than wave_max histories there (then one lane
     // per history, memo_search); heavy_mode 0 / 1 forces wave / lane
-    uint64_t heavy_mode = 2;
+    uint64_t heavy_mode = 1;
     uint64_t wave_max = 16384;
     bool lane_mode = false;
     uint32_t* probe_host = nullptr;    // pinned: [defer, heavy32, heavy64, giant] of the last finished call
@@ -291,6 +293,10 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "giant_grid") {
         if (value > 65536) return fail(c, QSMD_ERR_ARG, "giant_grid in 0..65536");
         c->giant_grid = value;
+    } else if (n == "wave_min_rem") {
+        c->wave_min_rem = std::min<uint64_t>(value, 0xFFFFFFFFull);
+    } else if (n == "wave_stats_ptr") {     // diagnostic: device buffer of 8 x u64 per wave_search workgroup
+        c->wave_stats = reinterpret_cast<unsigned long long*>(value);
     } else if (n == "heavy_mode") {
         if (value > 2) return fail(c, QSMD_ERR_ARG, "heavy_mode: 0 = wave, 1 = lane, 2 = auto");
         c->heavy_mode = value;
@@ -517,6 +523,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         wp.next64 = cnt + C_NEXT64;
         wp.budget = c->wave_budget;
         wp.explore_cap = cap;
+        wp.stats = c->wave_stats;
+        wp.memo_min_rem = (uint32_t)c->wave_min_rem;
         if (max_nodes) {
             const uint64_t mcap = 16 * max_nodes + 64 * c->wave_budget;
             wp.explore_cap = wp.explore_cap ? std::min(wp.explore_cap, mcap) : mcap;

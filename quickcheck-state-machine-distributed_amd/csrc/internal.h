@@ -212,6 +212,7 @@ struct WaveArgs {
     uint32_t* next64;
     uint64_t budget;              // nodes a task searches before it may split
     uint64_t explore_cap;         // iterations per history before the giant stage (0 = none)
+    uint32_t memo_min_rem;        // nodes with at most this many events left are not memoised
     unsigned long long* stats;    // diagnostic: 8 x u64 per workgroup (null in production)
 };
 hipError_t launch_wave(const WaveArgs& p, uint32_t grid, hipStream_t s);

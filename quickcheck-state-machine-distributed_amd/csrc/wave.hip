@@ -254,7 +254,7 @@ __device__ __forceinline__ void wave_insert(uint32_t* tab, const WKey& k, uint32
 template <uint32_t MODEL, class G, int MODE>
 __device__ __forceinline__ int wave_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* hist,
                                          int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* entry,
-                                         bool& skip, uint32_t* tab) {
+                                         bool& skip, uint32_t* tab, uint32_t min_rem) {
     using M = typename G::M;
     const bool empty = d.cand == (M)0;
     const bool term = empty & ((d.found == 0u) | (d.depth == d.base));
@@ -263,7 +263,7 @@ __device__ __forceinline__ int wave_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     if (empty & !term) {
         // leaving the node at depth d.depth (> base): its subtree was searched
         // to the end by this lane and failed (counts exact below 2^32)
-        if (!skip && d.nodes <= 0xFFFFFFFFull) {
+        if (!skip && d.nodes <= 0xFFFFFFFFull && (uint32_t)__builtin_popcountll((uint64_t)d.rem) > min_rem) {
             const WKey k = wave_key<MODEL, G>(d, a, s_bal, lane);
             if (k.ok) wave_insert(tab, k, (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES], lane);
         }
@@ -275,7 +275,7 @@ __device__ __forceinline__ int wave_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     if (d.cand) {
         const uint32_t dep0 = d.depth;
         status = d.template try_next<1, MODE>(a, hist, s_bal, lane, limit);
-        if (d.depth > dep0) {                     // entered a new node
+        if (d.depth > dep0 && (uint32_t)__builtin_popcountll((uint64_t)d.rem) > min_rem) {   // entered a new node
             entry[dep0 * C_LANES] = (uint32_t)d.nodes;
             const WKey k = wave_key<MODEL, G>(d, a, s_bal, lane);
             uint32_t c = 0;
@@ -314,7 +314,8 @@ __device__ void wave_history(const WaveArgs& p, uint32_t h, const qsmd_hdr& H, c
     uint64_t prefix_sum = 0, explored = 0;
     uint32_t best_status = QSMD_STATUS_NONLINEARISABLE, best_depth = 0, work = 0;
     bool incomplete = false, timed = false, skipped = false, overflow = false;
-    uint32_t tick = 0;
+    uint32_t tick = 0, n_splits = 0, n_hits = 0;
+    const uint64_t c0 = p.stats ? __builtin_amdgcn_s_memtime() : 0;
 
     // record the finished task of every lane with `done` (wave-synchronous)
     auto record = [&](bool done, uint64_t nodes) {
@@ -417,7 +418,8 @@ __device__ void wave_history(const WaveArgs& p, uint32_t h, const qsmd_hdr& H, c
         // ---- one DFS iteration on every busy lane
         int st = -1;
         if (busy) {
-            st = wave_step<MODEL, G, MODE>(dfs, a, L.hist, L.bal, lane, limit, &L.entry[0][lane], skip, tab);
+            st = wave_step<MODEL, G, MODE>(dfs, a, L.hist, L.bal, lane, limit, &L.entry[0][lane], skip, tab,
+                                           p.memo_min_rem);
             ++work;
             if (st < 0 && best.less(key)) st = QSMD_STATUS_SKIPPED;   // cancelled
         }
@@ -499,7 +501,10 @@ __device__ void wave_history(const WaveArgs& p, uint32_t h, const qsmd_hdr& H, c
             dfs.cand |= (M)1 << dfs.last_j;      // search on (a memo hit may have jumped past the limit)
             limit = dfs.nodes + p.budget;
         }
-        if (tot && room) pool_n += tot;          // the ranges of the lanes that split
+        if (tot && room) {
+            pool_n += tot;                       // the ranges of the lanes that split
+            ++n_splits;
+        }
         // ---- finished tasks: records, the best decider
         // (a BUDGET return is always a task budget: the caller's max_nodes is
         // applied by the fold)
@@ -554,6 +559,15 @@ __device__ void wave_history(const WaveArgs& p, uint32_t h, const qsmd_hdr& H, c
             status = QSMD_STATUS_BUDGET;
             nodes = a.max_nodes;
         }
+    }
+    if (p.stats && lane == 0) {                  // diagnostic
+        unsigned long long* q = p.stats + (uint64_t)blockIdx.x * 8;
+        q[0] += 1;
+        q[1] += tick;
+        q[2] += __builtin_amdgcn_s_memtime() - c0;
+        q[3] += n_splits;
+        q[4] = q[4] > tick ? q[4] : tick;
+        q[7] += nodes;
     }
     if (lane == 0) {
         if (status == QSMD_STATUS_HANDED_OFF) {  // the giant stage searches it again, from the root

@@ -81,7 +81,7 @@ def test_random_any_shape(ctx, model):
     _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
 
 
-DEFAULTS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 2, "wave_budget": 16, "wave_max": 16384,
+DEFAULTS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 1, "wave_budget": 16, "wave_max": 16384,
             "split_budget": 1024, "memo_lane_entries": 256, "memo_grid": 2048, "split_xmemo": 1}
 
 
@@ -241,7 +241,7 @@ def test_heavy_mode_auto_switches(ctx, knobs):
     """heavy_mode 2 (the default) picks wave or lane mode from the routing of
     the last finished call; results are exact whichever it picks and across
     the switches (bug-heavy batch, a clean one, the bug-heavy again)."""
-    knobs(wave_max=1000)
+    knobs(heavy_mode=2, wave_max=1000)
     b3 = gen.generate_config("bank_4x16_bugs", 11, 30000)
     b2 = gen.generate_config("bank_4x16", 11, 30000)
     for hdr, ev, _ in (b3, b3, b3, b2, b2, b3):
