@@ -1,0 +1,127 @@
+"""The multi-GPU driver (qsmd/dist.py) on the HIP kernels: two processes on
+cuda:0 with the gloo backend, each with its own device.Context -- the batch
+shards of SURVEY.md §8e (check_sharded with device_checker) and one history
+split at its root frontier over the ranks (check_single_split).  On an
+8-GPU node the same code runs one process per GPU over nccl (RCCL); that
+scaling run is the driver's, not this test's."""
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _paths():
+    sys.path[:0] = [os.path.join(HERE, "..", "quickcheck-state-machine-distributed_amd"),
+                    os.path.join(HERE, "..", "oracle"), HERE]
+
+
+def _heaviest(name, k, n=4000):
+    import oracle_c
+    from qsmd import gen
+    hdr, ev, _ = gen.generate_config(name, 0, n)
+    mid = gen.CONFIGS[name]["model_id"]
+    st, nd, _ = oracle_c.check_batch(mid, hdr, ev, threads=4, max_nodes=10**7)
+    out = []
+    for i in np.argsort(-nd.astype(np.int64))[:k]:
+        h = hdr[i:i + 1].copy()
+        a, m = int(h[0]["ev_off"]), int(h[0]["n_ev"])
+        h[0]["ev_off"] = 0
+        out.append((mid, h, ev[a:a + m].copy()))
+    return out
+
+
+def _worker(rank, world, port, n_total, out_q):
+    _paths()
+    import torch
+    import torch.distributed as dist
+
+    from qsmd import device, gen
+    from qsmd import dist as qdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    ctx = device.Context(0, time_limit_ms=60000)
+    try:
+        res = {}
+        p = gen.params(**gen.CONFIGS["bank_4x16_bugs"])
+        tot, stop, (first, count), st, nd = qdist.check_sharded(qdist.device_checker(ctx, max_nodes=10**7), p,
+                                                                n_total, rank, world)
+        res["shard"] = (tot.tolist(), stop, first, count, st.tolist(), [int(x) for x in nd])
+        splits = []
+        for mid, h, e in _heaviest("bank_4x16_bugs", 3):
+            s, nodes, w, info = qdist.check_single_split(ctx, mid, h, e, rank, world, tasks_per_rank=16)
+            splits.append((int(s), int(nodes), None if w is None else [int(x) for x in w], info["searched_here"]))
+        for bug in (True, False):
+            h, e, _ = gen.adversarial_ticket(8, 64, bug=bug)
+            s, nodes, w, info = qdist.check_single_split(ctx, 1, h, e, rank, world, tasks_per_rank=16,
+                                                         flags=device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_MEMO)
+            splits.append((int(s), int(nodes), None if w is None else [int(x) for x in w], info["searched_here"]))
+        res["split"] = splits
+        out_q.put((rank, res))
+    finally:
+        ctx.close()
+        dist.destroy_process_group()
+
+
+def test_two_processes_on_the_hip_kernels():
+    import oracle_c
+    from qsmd import dist as qdist
+    from qsmd import gen
+
+    world, n_total = 2, 20001
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # batch shards: every rank holds the global totals; the shards are the oracle's
+    hdr, ev, _ = gen.generate(gen.params(**gen.CONFIGS["bank_4x16_bugs"]), 0, n_total)
+    st_o, nd_o, _ = oracle_c.check_batch(gen.CONFIGS["bank_4x16_bugs"]["model_id"], hdr, ev, threads=8,
+                                         max_nodes=10**7)
+    want = qdist.totals_from_status(st_o, nd_o).tolist()
+    for r in range(world):
+        assert results[r]["shard"][0] == want
+    cat_st = np.array(results[0]["shard"][4] + results[1]["shard"][4])
+    cat_nd = np.array(results[0]["shard"][5] + results[1]["shard"][5])
+    assert np.array_equal(cat_st, st_o) and np.array_equal(cat_nd, nd_o.astype(np.int64))
+    # single histories split over the two ranks: the single search's verdict,
+    # count and witness (exhaustive); the memo mode's verdict for 8 x 64
+    for j, (mid, h, e) in enumerate(_heaviest("bank_4x16_bugs", 3)):
+        s_o, n_o, w_o = oracle_c.check_batch(mid, h, e, witness=True)
+        for r in range(world):
+            s, nodes, w, _ = results[r]["split"][j]
+            assert (s, nodes) == (int(s_o[0]), int(n_o[0]))
+            if s == 1:
+                assert w == [int(x) for x in w_o[:len(w)]]
+        assert results[0]["split"][j][3] + results[1]["split"][j][3] > 0
+    for k, bug in enumerate((True, False)):
+        h, e, _ = gen.adversarial_ticket(8, 64, bug=bug)
+        s_o, _, w_o = oracle_c.check_batch(1, h, e, memo=True, witness=True)
+        for r in range(world):
+            s, _, w, _ = results[r]["split"][3 + k]
+            assert s == int(s_o[0]) == (0 if bug else 1)
+            if not bug:
+                assert w == [int(x) for x in w_o[:len(w)]]

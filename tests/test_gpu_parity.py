@@ -51,6 +51,20 @@ def test_kats_on_device(ctx):
             assert replay_witness(m, hist, res.witness_of(0)), name
 
 
+def test_wire_bytes_through_the_c_abi(ctx):
+    """SchedulerHistory payload bytes (the reference's wire format, built by
+    hand in tests/test_wire.py) -> qsmd.wire -> qsmd_check_batch: the KATs'
+    verdicts and node counts."""
+    from test_wire import KAT2_BYTES, KAT7_BYTES
+    from qsmd import wire
+    for payload, mid, kat in ((KAT2_BYTES, models.MODEL_TICKET, "KAT2_reference_example"),
+                              (KAT7_BYTES, models.MODEL_BANK, "KAT7_bank_concurrent")):
+        hdr, ev = wire.batch_arrays([payload] * 3, mid)
+        st, nd, _, _ = ctx.check_arrays(mid, hdr, ev)
+        _, _, status, nodes = KATS[kat]
+        assert [codec.STATUS_NAMES[int(s)] for s in st] == [status] * 3 and list(nd) == [nodes] * 3
+
+
 def test_linearisable_signature(ctx):
     """The reference signature: linearisable transition postcondition model0 history."""
     _, h2, _, _ = KATS["KAT2_reference_example"]

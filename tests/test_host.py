@@ -220,3 +220,42 @@ def test_oracle_memo_verdicts():
         h, e, _ = gen.adversarial_ticket(8, 64, bug=bug)
         st, _, _ = oracle_c.check_batch(1, h, e, memo=True)
         assert st[0] == (codec.STATUS_NONLIN if bug else codec.STATUS_LIN)
+
+
+def _c_params(header, name):
+    txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", header)).read(), flags=re.S)
+    m = re.search(r"\b" + name + r"\s*\(([^)]*)\)", txt)
+    params = [p for p in m.group(1).split(",") if p.strip() and p.strip() != "void"]
+    return len(params)
+
+
+def test_haskell_binding_matches_the_c_abi():
+    """hs/Linearisability/Device.hs is source only (no GHC here): check that
+    every `foreign import` names an exported symbol with the C prototype's
+    arity, and that the model instances use include/qsmd.h's codes."""
+    src = open(os.path.join(ROOT, "hs", "Linearisability", "Device.hs")).read()
+    imports = re.findall(r'foreign import ccall safe "(\w+)"\s*\n\s*(\w+)\s*::(.*?)\n(?=\S|\s*\n)', src, re.S)
+    assert {c for c, _, _ in imports} >= {"qsmd_open", "qsmd_check_batch", "qsmd_last_error"}
+    declared = _declared("qsmd.h")
+    for cname, _, sig in imports:
+        assert cname in declared, cname
+        sig = re.sub(r"--[^\n]*", "", sig)
+        assert sig.count("->") == _c_params("qsmd.h", cname), cname
+    hdr = open(os.path.join(ROOT, "include", "qsmd.h")).read()
+    code = lambda n: int(re.search(r"#define " + n + r"\s+(\d+)u", hdr).group(1))  # noqa: E731
+    inst = open(os.path.join(ROOT, "hs", "DeviceInstances.hs")).read()
+    for hs_name, c_name in (("OpenAccount", "OPEN_ACCOUNT"), ("Deposit", "DEPOSIT"), ("Withdraw", "WITHDRAW"),
+                            ("CheckBalance", "CHECK_BALANCE"), ("Transfer", "TRANSFER")):
+        assert re.search(r"Bank\." + hs_name + r"\b[^\n]*Invocation " + str(code("QSMD_BANK_" + c_name)), inst), hs_name
+    for hs_name, c_name in (("AccountCreated", "ACCOUNT_CREATED"), ("DepositMade", "DEPOSIT_MADE"),
+                            ("WithdrawalMade", "WITHDRAWAL_MADE"), ("TransferMade", "TRANSFER_MADE"),
+                            ("AccountAlreadyExists", "ACCOUNT_ALREADY_EXISTS"),
+                            ("AccountDoesntExist", "ACCOUNT_DOESNT_EXIST"),
+                            ("InsufficientFunds", "INSUFFICIENT_FUNDS"), ("Balance", "BALANCE")):
+        assert re.search(r"Bank\." + hs_name + r"\b[^\n]*-> \(" + str(code("QSMD_BANK_" + c_name)), inst), hs_name
+    assert re.search(r"TD\.TakeTicket\s*= Just \(Invocation " + str(code("QSMD_TICKET_TAKE_TICKET")), inst)
+    assert re.search(r"TD\.Reset\s*= Just \(Invocation " + str(code("QSMD_TICKET_RESET")), inst)
+    assert re.search(r"TD\.Number i\) = Just \(" + str(code("QSMD_TICKET_NUMBER")), inst)
+    assert re.search(r"TD\.Ok\s*= Just \(" + str(code("QSMD_TICKET_OK")), inst)
+    assert "qsmdModelBank   = " + str(code("QSMD_MODEL_BANK")) in src
+    assert "qsmdModelTicket = " + str(code("QSMD_MODEL_TICKET")) in src
