@@ -12,9 +12,12 @@ before the timed region.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-Rank 0 prints one JSON line.  The cpu_baseline leg (N=1, rank 0) times the C
-oracle (oracle/ref_cpu.c, the reference restated with the same semantics) on a
-bounded sample of the same batch on the host's cores.
+Rank 0 prints one JSON line.  At N = 1 it also reports (outside the timed
+region of `value`): the CPU baselines on the host's cores -- the C oracle
+(oracle/ref_cpu.c, the reference restated with the same semantics) on one
+thread and on every available core, and the literal list transliteration of
+src/Linearisability.hs (the reference-shaped point) on config 1 -- and
+bounded runs of BASELINE configs 1, 3, 4 and 5 (`extra.configs`).
 """
 
 import argparse
@@ -36,6 +39,9 @@ from qsmd import codec, device, gen  # noqa: E402
 METRIC = ("histories checked/sec (whole node) + search nodes/sec, "
           "4×16-op Bank, 1/2/4/8 GPU")
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md)
+SIMDS = 1024                   # 256 CUs x 4 SIMDs
+CLOCK_HZ = 2.4e9               # MI355X peak engine clock
+VALU_CYCLES = 2                # a wave64 VALU instruction on a SIMD32
 
 
 def log(*a):
@@ -54,9 +60,116 @@ def hbm_bytes(hdr):
     return int((16 + 8 * hdr["n_ev"].astype(np.int64) + 1 + 8).sum())
 
 
-def cpu_baseline(hdr, ev, model_id, target_s):
-    """Time the C oracle on the rank-0 batch, single thread, repeating whole
-    passes until at least target_s seconds of CPU work have been measured."""
+def host_cores():
+    """Threads this process may use on the host: the box's CPU share when set
+    (OMP_NUM_THREADS), else the affinity set."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(env))) if env and env.isdigit() else aff
+
+
+class InFlight:
+    """S calls in flight (one context, stream and output set per slot; step k
+    runs on slot k % S, so the next batch's stage 0 fills the compute units
+    the previous call's tail leaves idle).  With RCCL the counters of R rounds
+    of steps are all-reduced together, overlapping the next block."""
+
+    def __init__(self, dev, model_id, d_hdr, n, d_ev, n_ev, S, R, flags, use_dist, knobs, budget0):
+        self.dev, self.model_id, self.d_hdr, self.n, self.d_ev, self.n_ev = dev, model_id, d_hdr, n, d_ev, n_ev
+        self.S, self.B, self.flags = S, R * S, flags
+        self.ctxs = [device.Context(dev.index) for _ in range(S)]
+        for c in self.ctxs:
+            if budget0 >= 0:
+                c.set_stage0_budget(budget0)
+            for k, v in knobs:
+                c.set_param(k, v)
+        self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+        self.outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
+                     for _ in range(S)]
+        # counters: [block parity][step of the block][8]; a row is reused two blocks later
+        self.tot = torch.zeros(2, self.B, 8, dtype=torch.int64, device=dev)
+        self.use_dist = use_dist
+        self.comm = self.streams[S - 1] if use_dist else None   # RCCL adds its own stream: reuse a slot's
+        self.do_ar = use_dist and os.environ.get("QSMD_BENCH_NOAR") != "1"
+        self.done = [None, None]
+        self.k = 0
+        self.last = (0, 0)
+
+    def _allreduce(self, par):
+        for st_ in self.streams[:-1]:
+            self.comm.wait_stream(st_)
+        with torch.cuda.stream(self.comm):
+            dist.all_reduce(self.tot[par], op=dist.ReduceOp.SUM)
+            self.done[par] = torch.cuda.Event()
+            self.done[par].record(self.comm)
+
+    def step(self):
+        k = self.k
+        self.k += 1
+        i, row, par = k % self.S, k % self.B, (k // self.B) % 2
+        d_st, d_nd = self.outs[i]
+        with torch.cuda.stream(self.streams[i]):
+            if self.done[par] is not None:
+                self.streams[i].wait_event(self.done[par])
+            self.ctxs[i].check_device(self.model_id, self.d_hdr.data_ptr(), self.n, self.d_ev.data_ptr(), self.n_ev,
+                                      d_st.data_ptr(), d_nd.data_ptr(), None, self.tot[par, row].data_ptr(),
+                                      flags=self.flags, stream=self.streams[i].cuda_stream)
+        if self.do_ar and row == self.B - 1:
+            self._allreduce(par)
+        self.last = (i, row, par)
+
+    def drain(self):
+        if self.k % self.B:                  # a partial last block: reduce it, start the next one fresh
+            if self.do_ar:
+                self._allreduce(((self.k - 1) // self.B) % 2)
+            self.k = (self.k + self.B - 1) // self.B * self.B
+
+    def timed(self, steps, warmup):
+        for _ in range(warmup):
+            self.step()
+        self.drain()
+        torch.cuda.synchronize(self.dev)
+        if self.use_dist:
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        self.ctxs[0].timing_reset()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        self.drain()
+        torch.cuda.synchronize(self.dev)
+        if self.use_dist:
+            dist.barrier()
+        torch.cuda.synchronize(self.dev)
+        elapsed = time.perf_counter() - t0
+        if self.use_dist:
+            e = torch.tensor([elapsed], dtype=torch.float64, device=self.dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            elapsed = float(e.item())
+        return elapsed
+
+    def results(self):
+        i, row, par = self.last
+        st = self.outs[i][0].cpu().numpy()
+        nd = self.outs[i][1].cpu().numpy()
+        return st, nd, self.tot[par, row].cpu().numpy()
+
+    def close(self):
+        for c in self.ctxs:
+            c.close()
+
+
+def device_batch(name, first, n, dev):
+    hdr, ev, _ = gen.generate(gen.params(**gen.CONFIGS[name]), first, n, threads=min(16, host_cores()))
+    return hdr, ev, torch.from_numpy(hdr.view(np.uint8)).to(dev), torch.from_numpy(ev.view(np.uint8)).to(dev)
+
+
+def cpu_baselines(hdr, ev, model_id, target_s, mt_s):
+    """The C oracle on the rank-0 batch: one thread for >= target_s seconds
+    of whole passes, then every available core for >= mt_s seconds."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_c
     oracle_c.lib()
@@ -68,19 +181,80 @@ def cpu_baseline(hdr, ev, model_id, target_s):
         dt += time.perf_counter() - t
         nodes += float(nd.astype(np.float64).sum())
         passes += 1
-    n = len(hdr) * passes
-    # SURVEY.md §8d also asks for the same port on every host core (history shards per thread)
-    threads = min(16, os.cpu_count() or 1)
-    t = time.perf_counter()
-    oracle_c.check_batch(model_id, hdr, ev, threads=threads)
-    dt_mt = time.perf_counter() - t
-    return {"value": n / dt, "unit": "histories/s", "cores": 1, "kind": "port",
+    cores = host_cores()
+    mt_passes, dt_mt = 0, 0.0
+    while dt_mt < mt_s or mt_passes == 0:
+        t = time.perf_counter()
+        oracle_c.check_batch(model_id, hdr, ev, threads=cores)
+        dt_mt += time.perf_counter() - t
+        mt_passes += 1
+    return {"value": len(hdr) * passes / dt, "unit": "histories/s", "cores": 1, "kind": "port",
             "sample": f"{passes} pass(es) over the {len(hdr)} rank-0 histories, 1 thread, {dt:.1f} s, "
                       f"oracle/ref_cpu.c -O3 (reference semantics, no memo)",
             "nodes_per_sec": nodes / dt,
-            "multi_thread": {"value": len(hdr) / dt_mt, "cores": threads,
-                             "sample": f"1 pass over the {len(hdr)} histories, {threads} threads, {dt_mt:.2f} s"}}, \
-        st, nd, len(hdr)
+            "multi_thread": {"value": len(hdr) * mt_passes / dt_mt, "cores": cores,
+                             "sample": f"{mt_passes} pass(es) over the {len(hdr)} histories, {cores} threads "
+                                       f"(history shards), {dt_mt:.2f} s"}}, st, nd
+
+
+def reference_shaped(seconds):
+    """The literal list transliteration of src/Linearisability.hs:25-69
+    (oracle/linearise_lists.py: cons-list copies, filter1, findResponse, the
+    lazy forest, any / any') on BASELINE config 1, CPython, one thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import linearise_lists as ll
+    from qsmd import models
+    hdr, ev, _ = gen.generate_config("ticket_2x10", 0, 20000)
+    b = codec.Batch(models.TICKET, hdr, ev, [{i: i for i in range(int(h["n_pid"]))} for h in hdr],
+                    [{} for _ in hdr])
+    hs = [codec.decode_history(b, i) for i in range(len(hdr))]
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        ll.check("ticket", hs[done % len(hs)])
+        done += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "histories/s", "cores": 1, "kind": "port",
+            "sample": f"{done} checks of {len(hs)} ticket_2x10 histories (BASELINE config 1), {dt:.1f} s, "
+                      f"oracle/linearise_lists.py (literal list transliteration, CPython)"}
+
+
+def extra_configs(dev, S, knobs):
+    """Bounded runs of BASELINE configs 1, 3, 5 (same in-flight step as the
+    headline) and 4 (one adversarial 8 x 64 TicketDispenser history, memo
+    mode), each checked against the oracle on a sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_c
+    out = {}
+    for cfg_id, name, n, steps in ((1, "ticket_2x10", 1_000_000, 20), (3, "bank_4x16_bugs", 1_000_000, 10),
+                                   (5, "bank_6x24", 100_000, 20)):
+        hdr, ev, d_hdr, d_ev = device_batch(name, 0, n, dev)
+        mid = gen.CONFIGS[name]["model_id"]
+        run = InFlight(dev, mid, d_hdr, n, d_ev, len(ev), S, 1, device.QSMD_FLAG_EXHAUSTIVE, False, knobs, -1)
+        el = run.timed(steps, 3)
+        st, nd, tot = run.results()
+        s0, call = run.ctxs[0].timing_read()
+        run.close()
+        m = min(n, 50_000)
+        st_o, nd_o, _ = oracle_c.check_batch(mid, hdr[:m], ev, threads=host_cores(), max_nodes=0)
+        out[f"config{cfg_id}"] = {
+            "workload": name, "histories": n, "steps": steps, "histories_per_sec": n * steps / el,
+            "nodes_per_sec": float(tot[7]) * steps / el, "device_ms_call_mean": float(np.mean(call)),
+            "nonlinearisable": int(tot[2]), "mismatches_vs_oracle": int(((st[:m] != st_o) |
+                                                                        (nd[:m] != nd_o.astype(np.int64))).sum()),
+            "checked_vs_oracle": m}
+    h, e, _ = gen.adversarial_ticket(8, 64, bug=True)
+    ctx = device.Context(dev.index)
+    times = []
+    for _ in range(4):
+        t = time.perf_counter()
+        st, nd, _, _ = ctx.check_arrays(1, h, e, flags=device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_MEMO)
+        times.append(time.perf_counter() - t)
+    ctx.close()
+    st_o, _, _ = oracle_c.check_batch(1, h, e, memo=True)
+    out["config4"] = {"workload": "adversarial TicketDispenser 8x64 (one history, QSMD_FLAG_MEMO, host entry)",
+                      "ms_per_history": 1e3 * float(np.median(times[1:])), "verdict": int(st[0]),
+                      "verdict_matches_oracle": bool(int(st[0]) == int(st_o[0]))}
+    return out
 
 
 def main():
@@ -92,24 +266,21 @@ def main():
     ap.add_argument("--n-hist", type=int, default=1_000_000, help="histories per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--split-budget", type=int, default=None,
-                    help="per-lane node budget before the split stage (library default if unset)")
+    ap.add_argument("--no-extra", action="store_true", help="skip the extra BASELINE configs")
     ap.add_argument("--stage0-budget", type=int, default=None,
-                    help="fixed stage-0 node budget (the rest go to the memo stage); default 40 with calls in "
-                         "flight (the next batch hides the memo stage; tools/gpu/inflight_budget*.sh, "
-                         "profiles/r01/v7/inflight_budget_sweep.json), the adaptive cascade one call at a time; -1 = adaptive")
+                    help="stage-0 node budget (default 40 with calls in flight, the library's otherwise)")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
                     help="qsmd_set_param on every context (tuning; repeatable)")
     ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="calls in flight (one context + stream each): the next step's search overlaps the tail of "
-                         "the previous one; 0 = 3 on one GPU, 2 with RCCL (its stream takes one of the 4 hardware queues)")
+                    help="calls in flight (one context + stream each); 0 = 3 on one GPU, 2 with RCCL "
+                         "(its stream takes one of the 4 hardware queues)")
     ap.add_argument("--ar-rounds", type=int, default=16,
                     help="rounds of in-flight steps whose counters one RCCL all-reduce carries (N > 1)")
     ap.add_argument("--device-gen", action="store_true",
                     help="generate the batch on the GPU (qsmd_gen_batch_device; same histories as the host generator)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                    help="PMC summary written by profiles/profile.sh (for roofline.traffic)")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02", "stage0_pmc.json"),
+                    help="PMC summary of the stage-0 kernel (profiles/summarize_pmc.py) for the roofline fields")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -117,7 +288,6 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    # the counter all-reduce (QSMD_BENCH_DIST=1 exercises it on one rank too)
     use_dist = world > 1 or os.environ.get("QSMD_BENCH_DIST") == "1"
     if use_dist:
         dist.init_process_group("nccl", device_id=dev)
@@ -125,135 +295,63 @@ def main():
     cfg = dict(gen.CONFIGS[args.config])
     model_id = cfg["model_id"]
     n = args.n_hist
-    ctx = device.Context(local)
     t = time.perf_counter()
     if args.device_gen:                   # on-device generation (csrc/gen.hip), same stream as the host's
         per = 2 * cfg["n_ops"]
         d_hdr = torch.empty(n * 16, dtype=torch.uint8, device=dev)
         d_ev = torch.empty(n * per * 8, dtype=torch.uint8, device=dev)
-        ctx.gen_device(gen.params(**cfg), rank * n, n, d_hdr.data_ptr(), d_ev.data_ptr(),
-                       stream=torch.cuda.current_stream(dev).cuda_stream)
+        gctx = device.Context(local)
+        gctx.gen_device(gen.params(**cfg), rank * n, n, d_hdr.data_ptr(), d_ev.data_ptr(),
+                        stream=torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
+        gctx.close()
         hdr = d_hdr.cpu().numpy().view(codec.HDR_DTYPE)
         ev = d_ev.cpu().numpy().view(codec.EV_DTYPE)
     else:
-        hdr, ev, bug = gen.generate(gen.params(**cfg), rank * n, n, threads=min(16, os.cpu_count() or 1))
-        d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
-        d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
+        hdr, ev, d_hdr, d_ev = device_batch(args.config, rank * n, n, dev)
     log(f"[rank {rank}] generated {n} histories ({'device' if args.device_gen else 'host'}) "
         f"in {time.perf_counter() - t:.2f}s")
 
-    # S calls in flight (--inflight): one context, stream and output set per
-    # slot; step k runs on slot k % S, so the next batch's stage 0 fills the
-    # compute units the previous call's tail leaves idle.  Each step is the
-    # full search of the batch; a slot's steps are ordered on its stream.
     S = args.inflight if args.inflight > 0 else (2 if use_dist else 3)
-    ctxs = [ctx] + [device.Context(local) for _ in range(S - 1)]
     budget0 = args.stage0_budget if args.stage0_budget is not None else (40 if S > 1 else -1)
-    for c in ctxs:
-        if args.split_budget is not None:
-            c.set_split_budget(args.split_budget)
-        if budget0 >= 0:
-            c.set_stage0_budget(budget0)
-        for kv in args.param:
-            name, value = kv.split("=")
-            c.set_param(name, int(value))
+    knobs = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in args.param]
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
-    outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
-            for _ in range(S)]
-    # counters: [block parity][step of the block][8]; a block is R rounds of S
-    # steps (--ar-rounds), all-reduced together (one bucketed RCCL all-reduce
-    # per block, overlapping the next block; a row is reused two blocks later,
-    # after it)
-    R = max(1, args.ar_rounds)
-    B = R * S
-    tot = torch.zeros(2, B, 8, dtype=torch.int64, device=dev)
-    # (the round's all-reduce runs on the last slot's stream: RCCL adds its own
-    # stream, and more streams than hardware queues serialise each other)
-    comm = streams[S - 1] if use_dist else None
-    do_ar = use_dist and os.environ.get("QSMD_BENCH_NOAR") != "1"   # (diagnostic: group without collectives)
-    done = [None, None]                   # per parity: the round's all-reduce finished
-    k_step = [0]
+    run = InFlight(dev, model_id, d_hdr, n, d_ev, len(ev), S, max(1, args.ar_rounds), flags, use_dist, knobs,
+                   budget0)
+    elapsed = run.timed(args.steps, args.warmup)
+    s0_ms, call_ms = run.ctxs[0].timing_read()
+    st, nd, tot = run.results()
+    run.close()
 
-    def step():
-        k = k_step[0]
-        k_step[0] += 1
-        i, row, par = k % S, k % B, (k // B) % 2
-        d_st_i, d_nd_i = outs[i]
-        with torch.cuda.stream(streams[i]):
-            if done[par] is not None:
-                streams[i].wait_event(done[par])
-            ctxs[i].check_device(model_id, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st_i.data_ptr(),
-                                 d_nd_i.data_ptr(), None, tot[par, row].data_ptr(), flags=flags,
-                                 stream=streams[i].cuda_stream)
-        if do_ar and row == B - 1:        # the block is enqueued: its counters all-reduced together
-            for st_ in streams[:-1]:
-                comm.wait_stream(st_)
-            with torch.cuda.stream(comm):
-                dist.all_reduce(tot[par], op=dist.ReduceOp.SUM)
-                done[par] = torch.cuda.Event()
-                done[par].record(comm)
-        return row, par
-
-    def drain():
-        if k_step[0] % B:                 # a partial last block: reduce it, start the next one fresh
-            if do_ar:
-                par = ((k_step[0] - 1) // B) % 2
-                for st_ in streams[:-1]:
-                    comm.wait_stream(st_)
-                with torch.cuda.stream(comm):
-                    dist.all_reduce(tot[par], op=dist.ReduceOp.SUM)
-                    done[par] = torch.cuda.Event()
-                    done[par].record(comm)
-            k_step[0] = (k_step[0] + B - 1) // B * B
-
-    for _ in range(args.warmup):
-        step()
-    drain()
-    torch.cuda.synchronize(dev)
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ctx.timing_reset()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        last = step()
-    drain()
-    torch.cuda.synchronize(dev)
-    if use_dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if use_dist:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-
-    s0_ms, call_ms = ctx.timing_read()
-    d_st, d_nd = outs[last[0] % S]
-    st = d_st.cpu().numpy()
-    nd = d_nd.cpu().numpy()
-    tot = tot[last[1], last[0]].cpu().numpy()   # global totals of the last step
     ms_per_step = elapsed / args.steps * 1e3
     total_hist = n * world
     value = total_hist * args.steps / elapsed
     nodes_total = int(tot[7])
     assert int(tot[0]) + int(tot[4]) + int(tot[5]) == total_hist, tot
 
-    # roofline of the dominant kernel (stage 0 search), rank-local
+    # roofline of the dominant kernel (stage 0), rank-local: algorithmic bytes
+    #  over its live HIP-event time; beside it the fractions the
+    # PMC counters of a profiling run of the same configuration give for the
+    # same live time: HBM bytes actually moved, and VALU issue
     s0_mean = float(np.mean(s0_ms)) if len(s0_ms) else float("nan")
-    # (with a fixed stage-0 budget the kernel stops a history at that many
-    # nodes and the memo stage searches it again: stage 0's own node work is
-    # min(nodes, budget) per history)
+    t_s0 = s0_mean * 1e-3
     a_bytes = alg_bytes(hdr, np.minimum(nd, budget0) if budget0 > 0 else nd)
-    achieved = a_bytes / (s0_mean * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic):
-        with open(args.traffic) as f:
-            tr = json.load(f)
-        if tr.get("config") == args.config and tr.get("n_hist") == n:
-            traffic = tr.get("hbm_bytes_per_launch")
+    achieved = a_bytes / t_s0 / 1e9
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": a_bytes,
+            "hbm_io_bytes_per_launch": hbm_bytes(hdr), "kernel": "compact_search<Bank, G32> (stage 0)"}
+    if os.path.exists(args.pmc):
+        with open(args.pmc) as f:
+            pmc = json.load(f)
+        if pmc.get("config") == args.config and pmc.get("n_hist") == n:
+            tr = pmc.get("hbm_bytes_per_launch")
+            roof["traffic"] = tr
+            if tr:
+                roof["hbm_actual"] = tr / t_s0 / (HBM_PEAK_GBS * 1e9)
+            valu = pmc.get("valu_insts_per_launch")
+            if valu:
+                roof["valu_issue"] = valu * VALU_CYCLES / (SIMDS * CLOCK_HZ * t_s0)
+            roof["pmc_source"] = os.path.relpath(args.pmc, ROOT)
 
     out = {
         "metric": METRIC, "value": value, "unit": "histories/s", "n_gpus": world,
@@ -264,28 +362,30 @@ def main():
         "config": {"workload": args.config, "histories_per_gpu": n,
                    "clients": cfg["n_clients"], "ops": cfg["n_ops"],
                    "events_per_history": 2 * cfg["n_ops"], "parallelism": f"shard{world}", "calls_in_flight": S,
-                   "stage0_budget": budget0 if budget0 >= 0 else "adaptive",
-                   "allreduce_every_steps": B if use_dist else None, "mode": "memo" if args.memo else "exhaustive"},
+                   "stage0_budget": budget0 if budget0 >= 0 else "library default",
+                   "allreduce_every_steps": S * max(1, args.ar_rounds) if use_dist else None,
+                   "mode": "memo" if args.memo else "exhaustive"},
         "nodes_per_sec": nodes_total * args.steps / elapsed,
         "verdicts": {"checked": int(tot[0]), "linearisable": int(tot[1]),
                      "nonlinearisable": int(tot[2]), "model_errors": int(tot[3]),
                      "budget": int(tot[5])},
         "device_ms": {"stage0_mean": s0_mean, "call_mean": float(np.mean(call_ms)) if len(call_ms) else None},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "alg_bytes_per_launch": a_bytes, "hbm_io_bytes_per_launch": hbm_bytes(hdr),
-                     "kernel": "compact_search<Bank> (stage 0)"},
+        "roofline": roof,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb, st_o, nd_o, sample = cpu_baseline(hdr, ev, model_id, args.cpu_seconds)
+        cb, st_o, nd_o = cpu_baselines(hdr, ev, model_id, args.cpu_seconds, 2.0)
+        cb["reference_shaped"] = reference_shaped(5.0)
         out["cpu_baseline"] = cb
-        out["mismatches_vs_oracle"] = int(((st_o != st[:sample]) | (nd_o != nd[:sample].astype(np.uint64))).sum())
-        out["checked_vs_oracle"] = sample
+        if args.memo:                        # node counts are "explored" there: verdicts only
+            out["mismatches_vs_oracle"] = int((st_o != st).sum())
+        else:
+            out["mismatches_vs_oracle"] = int(((st_o != st) | (nd_o != nd.astype(np.uint64))).sum())
+        out["checked_vs_oracle"] = len(hdr)
+    if rank == 0 and world == 1 and not args.no_extra:
+        out["extra"] = {"configs": extra_configs(dev, S, knobs)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    for c in ctxs:
-        c.close()
     if use_dist:
         dist.destroy_process_group()
 

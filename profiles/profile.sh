@@ -10,7 +10,7 @@
 # crashes stops the script (nothing further runs on the GPU).
 OUT=${1:-gpurun_out/prof}
 shift || true
-ARGS=${@:-"--steps 5 --warmup 1 --no-cpu-baseline"}
+ARGS=${@:-"--steps 5 --warmup 1 --no-cpu-baseline --no-extra"}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 run() {  # name, rocprofv3 args...

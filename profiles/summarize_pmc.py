@@ -15,6 +15,7 @@ import sys
 from collections import defaultdict
 
 DOMINANT = "compact_search"
+GEOMETRY = "G32>"            # stage 0 (stage 0w is the G64 instance)
 
 
 def rows(path_glob):
@@ -30,7 +31,7 @@ def counters(out_dir, name):
     kname = {}
     for r in rows(os.path.join(out_dir, name, "**", "*counter_collection.csv")):
         k = r.get("Kernel_Name", "")
-        if DOMINANT not in k:
+        if DOMINANT not in k or GEOMETRY not in k:
             continue
         d = r.get("Dispatch_Id") or r.get("Correlation_Id")
         per[d][r["Counter_Name"]] += float(r["Counter_Value"])
@@ -46,7 +47,7 @@ def main(out_dir):
     stats = rows(os.path.join(out_dir, "trace", "**", "*kernel_stats.csv"))
     res["kernels"] = {r["Name"]: {"calls": int(r["Calls"]), "mean_ns": float(r["AverageNs"]),
                                   "pct": float(r["Percentage"])} for r in stats}
-    dur = [v["mean_ns"] for k, v in res["kernels"].items() if DOMINANT in k]
+    dur = [v["mean_ns"] for k, v in res["kernels"].items() if DOMINANT in k and GEOMETRY in k]
     res["dominant_mean_ns"] = dur[0] if dur else None
     f = counters(out_dir, "fetch").get("FETCH_SIZE")
     w = counters(out_dir, "write").get("WRITE_SIZE")
@@ -58,6 +59,9 @@ def main(out_dir):
     sq = counters(out_dir, "sq1")
     sq.update(counters(out_dir, "sq2"))
     res["sq"] = sq
+    res["valu_insts_per_launch"] = sq.get("SQ_INSTS_VALU")
+    res["lds_bank_conflict_cycles"] = sq.get("SQ_LDS_BANK_CONFLICT")
+    res["lds_active_inst"] = sq.get("SQ_ACTIVE_INST_LDS")
     if sq.get("SQ_WAVE_CYCLES"):
         wc = sq["SQ_WAVE_CYCLES"]
         res["wait_any_frac"] = sq.get("SQ_WAIT_ANY", 0) / wc
