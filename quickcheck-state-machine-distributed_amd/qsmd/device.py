@@ -14,7 +14,7 @@ import numpy as np
 from . import codec
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libqsmd.so")
+LIB_PATH = os.environ.get("QSMD_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libqsmd.so")   # (A/B builds: tools/ab.py)
 
 QSMD_FLAG_EXHAUSTIVE = 1
 QSMD_FLAG_MEMO = 2
