@@ -55,13 +55,56 @@ __device__ __forceinline__ int run_search(DFS& dfs, const SearchArgs& a, const u
     return status;
 }
 
+
+// Stage the histories of the `fresh` lanes (history h) into their LDS
+// columns and classify them: returns -2 (deferred to the next stage), -1
+// (dfs initialised: search it) or a final status (encode error, the empty
+// history, skipped).  When all 64 lanes are fresh with one common length
+// and back-to-back events, the block stages coalesced (stage_packed).
+// Every lane of the wavefront calls it (the deferral append is a ballot).
+template <uint32_t MODEL, class G>
+__device__ __forceinline__ int stage_fresh(const SearchArgs& a, bool fresh, uint32_t h, uint32_t (*s_ev)[C_LANES],
+                                           int32_t (*s_bal)[C_LANES], int lane, LaneDFS<MODEL, G>& dfs,
+                                           qsmd_hdr& H) {
+    using M = typename G::M;
+    if (fresh) H = a.hdr[h];
+    else H = qsmd_hdr{0, 0, 0, 0, 0, 0};
+    const uint32_t n_ev = H.n_ev, n_pid = H.n_pid;
+    const bool enc_ok = fresh && H.model_id == MODEL && n_ev <= QSMD_MAX_EVENTS && n_pid <= QSMD_MAX_PIDS &&
+                        (uint64_t)H.ev_off + n_ev <= a.n_events;
+    const bool small = enc_ok && n_ev <= (uint32_t)G::EV && n_pid <= 8u && a.m0_small;
+
+    StagedT<M> s{0, 0, 0, 0, 0, true, true, false};
+    // a block: the fresh histories (a prefix of the lanes) with the first
+    // one's length, back to back
+    const uint64_t F = __ballot(fresh);
+    const uint32_t N0 = __builtin_amdgcn_readfirstlane(n_ev);
+    const uint32_t off0 = __builtin_amdgcn_readfirstlane(H.ev_off);
+    const bool lane_uni = small && n_ev == N0 && H.ev_off == off0 + (uint32_t)lane * N0;
+    const bool packed = F != 0ull && __ballot(fresh && !lane_uni) == 0ull && N0 > 0u;
+    if (packed) stage_packed<MODEL, G>(a, N0, off0, (uint32_t)__builtin_popcountll(F), s_ev, lane);
+    else if (small) stage_lane<MODEL, G>(a, H, s_ev, lane);
+    if (small) finish_lane<G>(s_ev, lane, n_ev, n_pid, s);
+    s.ok = s.ok && enc_ok;
+
+    const bool defer = enc_ok && (!small || (s.ok && !s.fits));
+    wave_append(defer, h, a.defer_list, a.defer_count, lane);   // -> the next stage
+    if (!fresh || defer) return -2;          // (dfs untouched: the lane may be searching)
+    dfs.depth = 0;
+    dfs.nodes = 0;
+    if (!s.ok) return QSMD_STATUS_ENCODE_ERROR;
+    if (n_ev == 0) return QSMD_STATUS_LINEARISABLE;                 // src/Linearisability.hs:59
+    if (beyond_first_fail(a, h)) return QSMD_STATUS_SKIPPED;
+    dfs.init(s, a, s_bal, lane);
+    return -1;
+}
+
 // G32: direct over [0, n_hist) (stage 0).  G64: the same search for
 // histories of 33..64 events (u64 masks, 16 KB of LDS), run in list mode over
 // the histories stage 0 deferred (a.list).
 template <uint32_t MODEL, class G = G32>
 __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(SearchArgs a) {
     constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
-    using M = typename G::M;
     __shared__ uint32_t s_ev[G::EV][C_LANES];
     __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
 
@@ -79,45 +122,14 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
         const bool active = idx < total;
         const uint32_t h = active ? (a.list ? a.list[idx] : (uint32_t)idx) : 0u;
         qsmd_hdr H;
-        if (active) H = a.hdr[h];
-        else H = qsmd_hdr{0, 0, 0, 0, 0, 0};
-        const uint32_t n_ev = H.n_ev, n_pid = H.n_pid;
-        const bool enc_ok = active && H.model_id == MODEL && n_ev <= QSMD_MAX_EVENTS &&
-                            n_pid <= QSMD_MAX_PIDS && (uint64_t)H.ev_off + n_ev <= a.n_events;
-        const bool small = enc_ok && n_ev <= (uint32_t)G::EV && n_pid <= 8u && a.m0_small;
-
-        StagedT<M> s{0, 0, 0, 0, 0, true, true, false};
-        const uint32_t N0 = __builtin_amdgcn_readfirstlane(n_ev);
-        const uint32_t off0 = __builtin_amdgcn_readfirstlane(H.ev_off);
-        const bool lane_uni = active && small && n_ev == N0 && H.ev_off == off0 + (uint32_t)lane * N0;
-        const bool packed = __ballot(!lane_uni) == 0ull && N0 > 0u;
-        if (packed) stage_packed<MODEL, G>(a, N0, off0, s_ev, lane);
-        else if (small) stage_lane<MODEL, G>(a, H, s_ev, lane);
-        if (small) finish_lane<G>(s_ev, lane, n_ev, n_pid, s);
-        s.ok = s.ok && enc_ok;
-
-        const bool defer = enc_ok && (!small || (s.ok && !s.fits));
-        wave_append(defer, h, a.defer_list, a.defer_count, lane);   // -> the next stage
-        if (!active || defer) continue;
-
-        int status = -1;
         LaneDFS<MODEL, G> dfs;
-        dfs.depth = 0;
-        dfs.nodes = 0;
-        bool search = false;
-        if (!s.ok) {
-            status = QSMD_STATUS_ENCODE_ERROR;
-        } else if (n_ev == 0) {
-            status = QSMD_STATUS_LINEARISABLE;                       // :59
-        } else if (beyond_first_fail(a, h)) {
-            status = QSMD_STATUS_SKIPPED;
-        } else {
-            dfs.init(s, a, s_bal, lane);
-            search = true;
-        }
+        int status = stage_fresh<MODEL, G>(a, active, h, s_ev, s_bal, lane, dfs, H);
+        if (status == -2) continue;
+        const bool search = status == -1;
+        const uint32_t n_ev = H.n_ev;
         // one specialised loop per wavefront: paired when every searched
         // history of the wavefront is paired
-        if (__ballot(search && !s.paired) == 0ull) {
+        if (__ballot(search && !dfs.paired) == 0ull) {
             if (search) status = run_search<M_PAIRED>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
         } else {
             if (search) status = run_search<M_GENERAL>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
@@ -135,6 +147,7 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
     }
     cnt.flush(a.buckets, lane);
 }
+
 
 hipError_t launch_compact64(const SearchArgs& a, uint32_t grid, hipStream_t s) {
     if (a.model_id == QSMD_MODEL_BANK)

@@ -99,11 +99,26 @@ constexpr uint64_t bank_exp_table() {
     return t;
 }
 constexpr uint64_t kBankExp = bank_exp_table();
-// per request code: sign of the step on account a (Deposit +1, Withdraw and
-// Transfer -1, Open / CheckBalance 0); an absent account is created with the
-// money exactly when the sign is non-zero (insertWith, test/Bank.hs:96-97)
-constexpr uint32_t kBankNeg = (1u << QSMD_BANK_WITHDRAW) | (1u << QSMD_BANK_TRANSFER);
-constexpr uint32_t kBankPos = (1u << QSMD_BANK_DEPOSIT);
+// The same table folded to 3 bits x (code, sel) with sel = exists a for
+// OpenAccount and lookup a >= Just m otherwise (a 30-bit word: one v_bfe).
+constexpr uint32_t bank_exp2_table() {
+    uint32_t t = 0;
+    for (uint32_t code = 0; code < 5; ++code)
+        for (uint32_t sel = 0; sel < 2; ++sel) {
+            // Open: sel = exists a; otherwise sel = ge (which implies exists a)
+            const uint32_t exa = sel, ge = code == QSMD_BANK_OPEN_ACCOUNT ? 0u : sel;
+            t |= (uint32_t)((kBankExp >> (3 * (code * 4 + exa * 2 + ge))) & 7u) << (code * 6 + sel * 3);
+        }
+    return t;
+}
+constexpr uint32_t kBankExp2 = bank_exp2_table();
+// per request code, the sign of the step on account a as a 2-bit signed
+// field (Deposit +1, Withdraw and Transfer -1, Open / CheckBalance 0)
+constexpr uint32_t kBankSign = (1u << (2 * QSMD_BANK_DEPOSIT)) | (3u << (2 * QSMD_BANK_WITHDRAW)) |
+                               (3u << (2 * QSMD_BANK_TRANSFER));
+__device__ __forceinline__ int32_t bank_sign(uint32_t code) {
+    return __builtin_amdgcn_sbfe((int32_t)kBankSign, code * 2u, 2u);
+}
 
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -180,13 +195,17 @@ struct StackN {
         for (int q = 0; q + 1 < NW; ++q) w[q] = __builtin_amdgcn_alignbit(w[q + 1], w[q], 8u);
         w[NW - 1] >>= 8;
     }
+    // push v (< 256) when c: one v_perm per word with a per-lane byte
+    // selector (the shifted word when c, the word itself otherwise)
     __device__ __forceinline__ void push_if(bool c, uint32_t v) {
+        const uint32_t keep = 0x07060504u;
+        const uint32_t sel0 = c ? 0x06050400u : keep, sel = c ? 0x06050403u : keep;
         uint32_t n[NW];
-        n[0] = (w[0] << 8) | v;
+        n[0] = __builtin_amdgcn_perm(w[0], v, sel0);
 #pragma unroll
-        for (int q = 1; q < NW; ++q) n[q] = __builtin_amdgcn_alignbit(w[q], w[q - 1], 24u);
+        for (int q = 1; q < NW; ++q) n[q] = __builtin_amdgcn_perm(w[q], w[q - 1], sel);
 #pragma unroll
-        for (int q = 0; q < NW; ++q) w[q] = c ? n[q] : w[q];
+        for (int q = 0; q < NW; ++q) w[q] = n[q];
     }
 };
 
@@ -227,50 +246,69 @@ __device__ __forceinline__ void stage_lane(const SearchArgs& a, const qsmd_hdr& 
 // to its history's lane column.
 __device__ __forceinline__ uint32_t magic_div(uint32_t N0) { return (uint32_t)(0xFFFFFFFFull / N0) + 1u; }
 
-template <uint32_t MODEL, class G = G32>
-__device__ __forceinline__ void stage_packed(const SearchArgs& a, uint32_t N0, uint32_t off0,
-                                             uint32_t (*s_ev)[C_LANES], int lane) {
+// The block's loads go 4 x 16 B per lane at a time (the stage is bound by
+// VALU issue, not by these round trips: 8 or 16 at a time measured no
+// faster).  A power-of-two length (the common packed batch) maps block event
+// g to its history (= column) by a shift.
+template <uint32_t MODEL, class G, bool POW2>
+__device__ __forceinline__ void stage_packed_body(const SearchArgs& a, uint32_t N0, uint32_t off0, uint32_t nh,
+                                                  uint32_t (*s_ev)[C_LANES], int lane) {
     // history of block event g: exact for g < 2^16 (g * N0 < 2^21 << 2^32)
-    const uint32_t mg = magic_div(N0);
-    auto put = [&](uint32_t g, uint32_t lo, int32_t val) {
-        const uint32_t hh = __umulhi(g, mg);
-        s_ev[g - hh * N0][hh] = compress<MODEL, G>(lo, val);
+    const uint32_t mg = POW2 ? 0u : magic_div(N0);
+    const uint32_t sh = POW2 ? (uint32_t)__builtin_ctz(N0) : 0u;
+    auto col_of = [&](uint32_t g, uint32_t& e) {
+        const uint32_t hh = POW2 ? g >> sh : __umulhi(g, mg);
+        e = POW2 ? g & (N0 - 1u) : g - hh * N0;
+        return hh;
     };
-    const uint32_t total_ev = 64u * N0;
-    if ((off0 & 1u) == 0u) {
+    constexpr uint32_t U = 4;
+    const uint32_t total_ev = nh * N0;
+    if (((off0 | total_ev) & 1u) == 0u) {         // 16-B aligned start, whole 16-B pairs
         const uint4* blk = reinterpret_cast<const uint4*>(a.events + off0);
-        for (uint32_t k0 = 0; k0 < total_ev / 2u; k0 += 4u * 64u) {
-            uint4 x[4];
+        const uint32_t nq = total_ev / 2u;
+        for (uint32_t k0 = 0; k0 < nq; k0 += U * 64u) {
+            uint4 x[U];
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
+            for (uint32_t u = 0; u < U; ++u) {
                 const uint32_t q = k0 + u * 64u + (uint32_t)lane;
-                x[u] = q < total_ev / 2u ? blk[q] : make_uint4(0u, 0u, 0u, 0u);
+                x[u] = q < nq ? blk[q] : make_uint4(0u, 0u, 0u, 0u);
             }
 #pragma unroll
-            for (uint32_t u = 0; u < 4; ++u) {
+            for (uint32_t u = 0; u < U; ++u) {
                 const uint32_t q = k0 + u * 64u + (uint32_t)lane;
-                if (q < total_ev / 2u) {
-                    put(2u * q, x[u].x, (int32_t)x[u].y);
-                    put(2u * q + 1u, x[u].z, (int32_t)x[u].w);
-                }
+                uint32_t e0, e1;
+                const uint32_t c0 = col_of(2u * q, e0), c1 = col_of(2u * q + 1u, e1);
+                if (2u * q < total_ev) s_ev[e0][c0] = compress<MODEL, G>(x[u].x, (int32_t)x[u].y);
+                if (2u * q + 1u < total_ev) s_ev[e1][c1] = compress<MODEL, G>(x[u].z, (int32_t)x[u].w);
             }
         }
     } else {
         const uint2* blk = a.events + off0;
-        for (uint32_t k0 = 0; k0 < total_ev; k0 += 8u * 64u) {
-            uint2 x[8];
+        for (uint32_t k0 = 0; k0 < total_ev; k0 += 2u * U * 64u) {
+            uint2 x[2u * U];
 #pragma unroll
-            for (uint32_t u = 0; u < 8; ++u) {
+            for (uint32_t u = 0; u < 2u * U; ++u) {
                 const uint32_t g = k0 + u * 64u + (uint32_t)lane;
                 x[u] = g < total_ev ? blk[g] : make_uint2(0u, 0u);
             }
 #pragma unroll
-            for (uint32_t u = 0; u < 8; ++u) {
+            for (uint32_t u = 0; u < 2u * U; ++u) {
                 const uint32_t g = k0 + u * 64u + (uint32_t)lane;
-                if (g < total_ev) put(g, x[u].x, (int32_t)x[u].y);
+                uint32_t e;
+                const uint32_t c = col_of(g, e);
+                if (g < total_ev) s_ev[e][c] = compress<MODEL, G>(x[u].x, (int32_t)x[u].y);
             }
         }
     }
+}
+
+// nh histories packed back to back with one common length N0 from event
+// off0, history hh to column hh
+template <uint32_t MODEL, class G = G32>
+__device__ __forceinline__ void stage_packed(const SearchArgs& a, uint32_t N0, uint32_t off0, uint32_t nh,
+                                             uint32_t (*s_ev)[C_LANES], int lane) {
+    if ((N0 & (N0 - 1u)) == 0u) stage_packed_body<MODEL, G, true>(a, N0, off0, nh, s_ev, lane);
+    else stage_packed_body<MODEL, G, false>(a, N0, off0, nh, s_ev, lane);
 }
 
 // Per lane, over its own column: the encoding checks (markers, pid <
@@ -439,8 +477,7 @@ struct LaneDFS {
             // undo Transfer's deposit on b, then the step on a
             const int32_t rb = (pb | (ia == ib)) ? bb - m : 0;
             const int32_t cur_a = (tr & (ia == ib)) ? rb : ba;
-            const int32_t sa = (int32_t)((kBankPos >> code) & 1u) - (int32_t)((kBankNeg >> code) & 1u);
-            const int32_t ra = pa ? cur_a - sa * m : 0;
+            const int32_t ra = pa ? cur_a - bank_sign(code) * m : 0;
             const int32_t fb = tr ? rb : bb;
             s_bal[ib][lane] = fb;                  // a no-op unless Transfer
             s_bal[ia][lane] = ra;                  // written last (ia == ib)
@@ -513,31 +550,31 @@ struct LaneDFS {
             const int32_t bal_a = s_bal[ia][lane], bal_b = s_bal[ib][lane];
             const uint32_t ex_a = (ex >> ia) & 1u, ex_b = (ex >> ib) & 1u;
             // post (test/Bank.hs:118-131): invariant && expected response
-            const uint32_t tr = code == QSMD_BANK_TRANSFER ? 1u : 0u;
+            const bool tr = code == QSMD_BANK_TRANSFER;
             const bool chk = code == QSMD_BANK_CHECK_BALANCE;
-            const uint32_t ge = (ex_a & (bal_a >= m ? 1u : 0u));   // lookup >= Just m
-            const uint32_t exp = (uint32_t)(kBankExp >> (3u * (code * 4u + ex_a * 2u + ge))) & 7u;
+            const bool same = ia == ib;
+            // expected constructor: kBankExp2[code][exists a (Open) / lookup a >= Just m]
+            const uint32_t sel = ((code == QSMD_BANK_OPEN_ACCOUNT) | (bal_a >= m)) ? ex_a : 0u;
+            const uint32_t exp = __builtin_amdgcn_ubfe(kBankExp2, code * 6u + sel * 3u, 3u);
             const bool inv_ok = neg == 0u;
             err = has & inv_ok & chk & (rc == QSMD_BANK_BALANCE) & !ex_a;   // Map.! raises
             ok = has & !over & inv_ok & (rc == exp) & (!chk | (rv == bal_a));
-            // next' (test/Bank.hs:92-101) on a, then Transfer's deposit on b;
-            // stored unconditionally (the old values when !ok)
+            // next' (test/Bank.hs:92-101) on a (an absent account is created
+            // with m exactly when the step's sign is non-zero: insertWith),
+            // then Transfer's deposit on b; stored unconditionally (the old
+            // values when !ok)
             stw = j | (ex_a << JB) | (ex_b << (JB + 1u));
-            const int32_t sa = (int32_t)((kBankPos >> code) & 1u) - (int32_t)((kBankNeg >> code) & 1u);
-            const int32_t na = ex_a ? bal_a + sa * m : (sa != 0 ? m : 0);
-            const uint32_t ex1 = ex | ((chk ? 0u : 1u) << ia);
-            const int32_t bo = ia == ib ? na : bal_b;
-            const int32_t nb = ((ex1 >> ib) & 1u) ? bo + m : m;
-            const int32_t fb = tr ? nb : bo;
+            const int32_t sa = bank_sign(code);
+            const int32_t na = (ex_a ? bal_a : 0) + (ex_a ? sa : (sa & 1)) * m;
+            const int32_t bo = same ? na : bal_b;
+            const int32_t fb = tr ? (((ex_b != 0u) | same) ? bo : 0) + m : bo;
             s_bal[ia][lane] = ok ? na : bal_a;
             s_bal[ib][lane] = ok ? fb : bal_b;
-            const uint32_t ex2 = ex1 | (tr << ib);
-            const int32_t va = ia == ib ? fb : na;
-            // ok => neg == 0 before the step: only a and b can turn negative
-            uint32_t neg2 = ((va < 0) ? ((ex2 >> ia) & 1u) : 0u) << ia;
-            neg2 |= ((fb < 0) ? ((ex2 >> ib) & 1u) : 0u) << ib;
-            ex = ok ? ex2 : ex;
-            neg = ok ? neg2 : neg;
+            const int32_t va = same ? fb : na;
+            ex = ok ? (ex | ((chk ? 0u : 1u) << ia) | ((tr ? 1u : 0u) << ib)) : ex;
+            // ok => the invariant held before the step and absent accounts
+            // hold 0: the child breaks it iff a or b went negative
+            neg = ok ? (((va | fb) < 0) ? 1u : 0u) : neg;
         } else {
             // model at this depth: Just (#TT since the last Reset), or model0
             // advanced by succ <$> once per level
