@@ -17,9 +17,8 @@
 // failed subtree); only the work changes: 10^4-node Bank histories with
 // injected bugs take ~10^2 explored nodes.
 //
-// Table: one private table per lane -- G32: kLdsEntries entries in LDS;
-// G64: the lane's slot of the grid, T direct-mapped entries in HBM -- keyed
-// by the history index and the call's
+// Table: one private table per lane (the lane's slot in the grid), T
+// direct-mapped entries in HBM, keyed by the history index and the call's
 // epoch (stale entries never match, nothing is cleared per call) and the
 // full state: remaining-event mask and model (Bank: existing accounts and
 // their balances as i16; Ticket: Just n).  A state outside that encoding
@@ -97,37 +96,6 @@ __device__ __forceinline__ MemoKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d
     return k;
 }
 
-// G32: the lane's table in LDS, kLdsEntries direct-mapped entries, word w of
-// entry e at s_tab[e * 8 + w][lane] (each lane its own bank); an LDS probe
-// instead of an HBM round trip per node (the stage runs a few dozen
-// wavefronts, so 64 KB per wavefront costs no occupancy that matters).
-constexpr uint32_t kLdsEntries = 32;
-constexpr uint32_t kNoHistory = 0xFFFFFFFFu;   // word 0 of an empty entry (no history has this index)
-
-template <uint32_t MODEL, class G>
-__device__ __forceinline__ bool memo_lookup_lds(const uint32_t* col, const MemoKey<MODEL, G>& k, uint32_t h,
-                                                uint32_t& count) {
-    const uint32_t* e = col + (k.slot & (kLdsEntries - 1u)) * 8u * C_LANES;
-    bool hit = e[0] == h && e[1 * C_LANES] == k.w1 && e[2 * C_LANES] == k.rem_lo && e[4 * C_LANES] == k.m[0] &&
-               e[5 * C_LANES] == k.m[1] && e[6 * C_LANES] == k.m[2] && e[7 * C_LANES] == k.m[3];
-    count = e[3 * C_LANES];
-    return hit;
-}
-
-template <uint32_t MODEL, class G>
-__device__ __forceinline__ void memo_insert_lds(uint32_t* col, const MemoKey<MODEL, G>& k, uint32_t h,
-                                                uint32_t count) {
-    uint32_t* e = col + (k.slot & (kLdsEntries - 1u)) * 8u * C_LANES;
-    e[0] = h;
-    e[1 * C_LANES] = k.w1;
-    e[2 * C_LANES] = k.rem_lo;
-    e[3 * C_LANES] = count;
-    e[4 * C_LANES] = k.m[0];
-    e[5 * C_LANES] = k.m[1];
-    e[6 * C_LANES] = k.m[2];
-    e[7 * C_LANES] = k.m[3];
-}
-
 template <uint32_t MODEL, class G>
 __device__ __forceinline__ bool memo_lookup(const uint32_t* tab, const MemoKey<MODEL, G>& k, uint32_t h,
                                             uint32_t& count) {
@@ -150,7 +118,7 @@ __device__ __forceinline__ void memo_insert(uint32_t* tab, const MemoKey<MODEL, 
 
 // One DFS iteration with the memo (LaneDFS::step plus the two hooks).
 // entry: the lane's column of node counts at entry, per level.
-template <uint32_t MODEL, class G, int MODE, bool LDS>
+template <uint32_t MODEL, class G, int MODE>
 __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* evc,
                                          int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* tab,
                                          uint32_t h, uint32_t epoch, uint32_t mask, uint32_t* entry, bool& skip) {
@@ -165,10 +133,7 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
         if (!skip && d.nodes <= 0xFFFFFFFFull) {
             const uint32_t cnt = (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES];
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
-            if (k.ok) {
-                if constexpr (LDS) memo_insert_lds<MODEL, G>(tab, k, h, cnt);
-                else memo_insert<MODEL, G>(tab, k, h, cnt);
-            }
+            if (k.ok) memo_insert<MODEL, G>(tab, k, h, cnt);
         }
         skip = false;
         const uint32_t j = d.template undo<C_LANES, MODE>(evc, s_bal, lane);
@@ -182,12 +147,7 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
             entry[dep0 * C_LANES] = (uint32_t)d.nodes;
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             uint32_t cnt = 0;
-            bool hit = false;
-            if (k.ok) {
-                if constexpr (LDS) hit = memo_lookup_lds<MODEL, G>(tab, k, h, cnt);
-                else hit = memo_lookup<MODEL, G>(tab, k, h, cnt);
-            }
-            if (hit) {
+            if (k.ok && memo_lookup<MODEL, G>(tab, k, h, cnt)) {
                 if (d.nodes + cnt > limit) {      // the budget falls inside that subtree
                     d.nodes = limit;
                     status = QSMD_STATUS_BUDGET;
@@ -208,32 +168,22 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
 // list mode over a.list (the heavy histories of a compact stage); every
 // history of the list fits geometry G (it was staged there before)
 template <uint32_t MODEL, class G>
-__global__ __launch_bounds__(C_LANES, G::EV == 32 ? 1 : 2) void memo_search(MemoArgs p) {
+__global__ __launch_bounds__(C_LANES, G::EV == 32 ? 3 : 2) void memo_search(MemoArgs p) {
     constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
-    constexpr bool LDS = G::EV == 32;
     using M = typename G::M;
     const SearchArgs& a = p.s;
     __shared__ uint32_t s_ev[G::EV][C_LANES];
     __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
     __shared__ uint32_t s_entry[G::LEVELS][C_LANES];
-    __shared__ uint32_t s_tab[LDS ? kLdsEntries * 8 : 1][C_LANES];
 
     const int lane = threadIdx.x;
     const uint64_t total = *a.list_count;
     Counters cnt;
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
-    uint32_t* tab;
-    uint32_t mask;
-    if constexpr (LDS) {
-        tab = &s_tab[0][lane];
-        mask = kLdsEntries - 1u;
-        for (uint32_t e = 0; e < kLdsEntries; ++e) s_tab[e * 8u][lane] = kNoHistory;
-    } else {
-        tab = p.table + ((uint64_t)blockIdx.x * C_LANES + (uint64_t)lane) * (uint64_t)p.entries *
-                            (uint64_t)MemoEntry<G>::W;
-        mask = p.entries - 1u;
-    }
+    uint32_t* tab = p.table + ((uint64_t)blockIdx.x * C_LANES + (uint64_t)lane) * (uint64_t)p.entries *
+                                  (uint64_t)MemoEntry<G>::W;
+    const uint32_t mask = p.entries - 1u;
     for (uint64_t base = (uint64_t)blockIdx.x * C_LANES; base < total; base += (uint64_t)gridDim.x * C_LANES) {
         const uint64_t idx = base + lane;
         const bool active = idx < total;
@@ -266,8 +216,8 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 1 : 2) void memo_search(Memo
             bool skip = false;
             uint32_t iter = 0;
             do {
-                status = memo_step<MODEL, G, M_LANE, LDS>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, tab, h,
-                                                          p.epoch, mask, &s_entry[0][lane], skip);
+                status = memo_step<MODEL, G, M_LANE>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, tab, h, p.epoch,
+                                                     mask, &s_entry[0][lane], skip);
                 ++iter;
                 if (p.giant_cap && iter >= p.giant_cap && status < 0) {
                     status = QSMD_STATUS_HANDED_OFF;
