@@ -44,7 +44,8 @@ struct qsmd_ctx {
     hipEvent_t done_ev = nullptr;
     hipStream_t last_stream = nullptr;
     bool in_flight = false;
-    bool any_call = false;             // a check call was enqueued (its probe can be read)
+    bool any_call = false;             // a check call was enqueued
+    bool probe_valid = false;          // a check call finished: probe_host holds real counts
     // timing: per call, events before stage 0, after stage 0 and after the
     // giant stage, recorded on the launch stream (a ring of kTimingSlots)
     std::vector<hipEvent_t> ev;        // 3 per slot
@@ -375,6 +376,13 @@ static int memo_prepare(qsmd_ctx* c, hipStream_t s, unsigned long long** out) {
 // Lane mode's tables (3 GB by default), allocated on first use; false when
 // the device cannot hold them (the context then stays in wave mode: the same
 // results, a different speed).
+// A tail stage's grid: one workgroup per 64 histories the last call sent
+// there, between 2 per CU and `cap` (cap before the first call).
+static uint64_t tail_grid(const qsmd_ctx* c, uint64_t cap, uint64_t last) {
+    if (last == 0xFFFFFFFFull || last > 0xFFFFFFFFull) return cap;
+    return std::min<uint64_t>(cap, std::max<uint64_t>(2ull * c->n_cu, (last + 63) / 64));
+}
+
 static bool lane_tables(qsmd_ctx* c, hipStream_t s) {
     const size_t need = (size_t)c->memo_grid * 64 * c->mt_entries * (32 + 64);
     if (c->mt_failed) return false;
@@ -414,6 +422,12 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     else if (c->heavy_mode != 2)
         c->lane_mode = c->heavy_mode == 1;
     const bool lane = c->lane_mode && lane_tables(c, s);
+    // the tail launches' grids from the last finished call's list sizes (a
+    // hint: every tail kernel is grid-stride, any grid gives the same
+    // results); none before a call has finished
+    if (!c->probe_valid && c->any_call && hipEventQuery(c->done_ev) == hipSuccess) c->probe_valid = true;
+    uint32_t hint[4];
+    for (int i = 0; i < 4; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
 
     // ---- workspace: header, lists, giant records, tasks
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
@@ -490,7 +504,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     aw.heavy_list = h64;
     aw.heavy_count = cnt + C_HEAVY64;
     aw.stage0_budget = c->stage0w_budget ? c->stage0w_budget : ~0ull;
-    HIP_TRY(c, launch_compact64(aw, kStage0wGrid, s), "stage 0w launch");
+    HIP_TRY(c, launch_compact64(aw, (uint32_t)tail_grid(c, kStage0wGrid, hint[0]), s), "stage 0w launch");
     stage_done("stage0w", s, cnt);
     // ---- heavy stage: histories over the stage budgets
     const uint64_t cap = split ? 64 * c->split_budget : 0;
@@ -500,17 +514,20 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             ++c->mt_epoch;
         }
         const uint64_t slots = c->memo_grid * 64 * c->mt_entries;
+        MemoArgs mp[2]{};
         for (int w = 0; w < 2; ++w) {
-            MemoArgs mp{};
-            mp.s = a;
-            mp.s.list = w ? h64 : h32;
-            mp.s.list_count = cnt + (w ? C_HEAVY64 : C_HEAVY32);
-            mp.table = reinterpret_cast<uint32_t*>(c->mt + (w ? slots * 32 : 0));
-            mp.entries = (uint32_t)c->mt_entries;
-            mp.epoch = c->mt_epoch;
-            mp.giant_cap = cap;
-            HIP_TRY(c, launch_memo(mp, (uint32_t)c->memo_grid, w == 1, s), "memo launch");
+            mp[w].s = a;
+            mp[w].s.list = w ? h64 : h32;
+            mp[w].s.list_count = cnt + (w ? C_HEAVY64 : C_HEAVY32);
+            mp[w].table = reinterpret_cast<uint32_t*>(c->mt + (w ? slots * 32 : 0));
+            mp[w].entries = (uint32_t)c->mt_entries;
+            mp[w].epoch = c->mt_epoch;
+            mp[w].giant_cap = cap;
         }
+        // G64 groups in this launch only when the last call had some (else they go to the giant stage)
+        const bool wide = hint[2] != 0u;
+        HIP_TRY(c, launch_memo(mp[0], mp[1], (uint32_t)tail_grid(c, c->memo_grid, (uint64_t)hint[1] + hint[2]), wide, s),
+                "memo launch");
         stage_done("lane", s, cnt);
     } else {
         WaveArgs wp{};
@@ -572,7 +589,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         p.memo_exact = 1;
         p.memo_epoch = c->xm_epoch;
     }
-    const uint64_t gg = c->giant_grid ? c->giant_grid : 2ull * c->n_cu;
+    const uint64_t gg = c->giant_grid ? c->giant_grid
+                                      : (early || hint[3] ? 2ull * c->n_cu : 64ull);
     if (sync_stages()) {
         if (!c->debug_host)
             (void)hipHostMalloc(reinterpret_cast<void**>(&c->debug_host), 65536 * 16, hipHostMallocMapped | hipHostMallocCoherent);

@@ -227,7 +227,7 @@ struct MemoArgs {
     uint32_t epoch;               // this call's tag (24 bits)
     uint64_t giant_cap;           // > 0: a search past this many iterations goes to s.giant_list
 };
-hipError_t launch_memo(const MemoArgs& p, uint32_t grid, bool wide, hipStream_t s);
+hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s);
 
 hipError_t launch_gen(const qsmd_gen_params& p, uint64_t first, uint64_t n_hist, uint32_t ev_base, qsmd_hdr* hdr,
                       qsmd_event* events, uint8_t* bug_out, hipStream_t s);

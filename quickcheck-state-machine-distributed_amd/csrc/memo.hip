@@ -165,94 +165,124 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
 
 }  // namespace
 
-// list mode over a.list (the heavy histories of a compact stage); every
-// history of the list fits geometry G (it was staged there before)
+namespace {
+
 template <uint32_t MODEL, class G>
-__global__ __launch_bounds__(C_LANES, G::EV == 32 ? 3 : 2) void memo_search(MemoArgs p) {
-    constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
+struct MemoLds {
+    uint32_t ev[G::EV][C_LANES];
+    int32_t bal[MODEL == QSMD_MODEL_BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
+    uint32_t entry[G::LEVELS][C_LANES];   // node count at entry, per level
+};
+
+// One group of 64 histories of p's list (from index base); every history of
+// the list fits geometry G (a compact stage staged it before).
+template <uint32_t MODEL, class G>
+__device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, MemoLds<MODEL, G>& L, Counters& cnt,
+                                           uint64_t t0, int lane) {
     using M = typename G::M;
     const SearchArgs& a = p.s;
-    __shared__ uint32_t s_ev[G::EV][C_LANES];
-    __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
-    __shared__ uint32_t s_entry[G::LEVELS][C_LANES];
-
-    const int lane = threadIdx.x;
     const uint64_t total = *a.list_count;
-    Counters cnt;
-    const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
     uint32_t* tab = p.table + ((uint64_t)blockIdx.x * C_LANES + (uint64_t)lane) * (uint64_t)p.entries *
                                   (uint64_t)MemoEntry<G>::W;
     const uint32_t mask = p.entries - 1u;
-    for (uint64_t base = (uint64_t)blockIdx.x * C_LANES; base < total; base += (uint64_t)gridDim.x * C_LANES) {
-        const uint64_t idx = base + lane;
-        const bool active = idx < total;
-        const uint32_t h = active ? a.list[idx] : 0u;
-        qsmd_hdr H;
-        if (active) H = a.hdr[h];
-        else H = qsmd_hdr{0, 0, 0, 0, 0, 0};
-        StagedT<M> s{0, 0, 0, 0, 0, true, true, false};
-        if (active) {
-            stage_lane<MODEL, G>(a, H, s_ev, lane);
-            finish_lane<G>(s_ev, lane, H.n_ev, H.n_pid, s);
-        }
-        if (!active) continue;
-        int status = -1;
-        LaneDFS<MODEL, G> dfs;
-        dfs.depth = 0;
-        dfs.nodes = 0;
-        bool search = false;
-        if (!s.ok || !s.fits) {
-            status = QSMD_STATUS_ENCODE_ERROR;   // cannot happen: the list came from a compact stage
-        } else if (H.n_ev == 0) {
-            status = QSMD_STATUS_LINEARISABLE;
-        } else if (beyond_first_fail(a, h)) {
-            status = QSMD_STATUS_SKIPPED;
-        } else {
-            dfs.init(s, a, s_bal, lane);
-            search = true;
-        }
-        if (search) {
-            bool skip = false;
-            uint32_t iter = 0;
-            do {
-                status = memo_step<MODEL, G, M_LANE>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, tab, h, p.epoch,
-                                                     mask, &s_entry[0][lane], skip);
-                ++iter;
-                if (p.giant_cap && iter >= p.giant_cap && status < 0) {
-                    status = QSMD_STATUS_HANDED_OFF;
-                } else if ((iter & 1023u) == 0u && status < 0) {
-                    if (beyond_first_fail(a, h)) {
-                        status = QSMD_STATUS_SKIPPED;
-                    } else if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
-                        atomicOr(a.timed_out, 1u);
-                        status = QSMD_STATUS_BUDGET;
-                    }
-                }
-            } while (status < 0);
-        }
-        if (status == QSMD_STATUS_HANDED_OFF) {  // the giant stage searches it (exact, from the root)
-            a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
-            continue;
-        }
-        note_failure(a, h, status);
-        a.status[h] = (uint8_t)status;
-        if (a.nodes) a.nodes[h] = dfs.nodes;
-        if (a.witness && status == QSMD_STATUS_LINEARISABLE) dfs.write_witness(a.witness + H.ev_off, H.n_ev);
-        cnt.add(status, dfs.nodes);
+    const uint64_t idx = base + lane;
+    const bool active = idx < total;
+    const uint32_t h = active ? a.list[idx] : 0u;
+    qsmd_hdr H;
+    if (active) H = a.hdr[h];
+    else H = qsmd_hdr{0, 0, 0, 0, 0, 0};
+    StagedT<M> s{0, 0, 0, 0, 0, true, true, false};
+    if (active) {
+        stage_lane<MODEL, G>(a, H, L.ev, lane);
+        finish_lane<G>(L.ev, lane, H.n_ev, H.n_pid, s);
     }
-    cnt.flush(a.buckets, lane);
+    if (!active) return;
+    int status = -1;
+    LaneDFS<MODEL, G> dfs;
+    dfs.depth = 0;
+    dfs.nodes = 0;
+    bool search = false;
+    if (!s.ok || !s.fits) {
+        status = QSMD_STATUS_ENCODE_ERROR;   // cannot happen: the list came from a compact stage
+    } else if (H.n_ev == 0) {
+        status = QSMD_STATUS_LINEARISABLE;
+    } else if (beyond_first_fail(a, h)) {
+        status = QSMD_STATUS_SKIPPED;
+    } else {
+        dfs.init(s, a, L.bal, lane);
+        search = true;
+    }
+    if (search) {
+        bool skip = false;
+        uint32_t iter = 0;
+        do {
+            status = memo_step<MODEL, G, M_LANE>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch, mask,
+                                                 &L.entry[0][lane], skip);
+            ++iter;
+            if (p.giant_cap && iter >= p.giant_cap && status < 0) {
+                status = QSMD_STATUS_HANDED_OFF;
+            } else if ((iter & 1023u) == 0u && status < 0) {
+                if (beyond_first_fail(a, h)) {
+                    status = QSMD_STATUS_SKIPPED;
+                } else if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
+                    atomicOr(a.timed_out, 1u);
+                    status = QSMD_STATUS_BUDGET;
+                }
+            }
+        } while (status < 0);
+    }
+    if (status == QSMD_STATUS_HANDED_OFF) {      // the giant stage searches it (exact, from the root)
+        a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
+        return;
+    }
+    note_failure(a, h, status);
+    a.status[h] = (uint8_t)status;
+    if (a.nodes) a.nodes[h] = dfs.nodes;
+    if (a.witness && status == QSMD_STATUS_LINEARISABLE) dfs.write_witness(a.witness + H.ev_off, H.n_ev);
+    cnt.add(status, dfs.nodes);
 }
 
-hipError_t launch_memo(const MemoArgs& p, uint32_t grid, bool wide, hipStream_t s) {
-    const bool bank = p.s.model_id == QSMD_MODEL_BANK;
-    if (wide) {
-        if (bank) hipLaunchKernelGGL((memo_search<QSMD_MODEL_BANK, G64>), dim3(grid), dim3(C_LANES), 0, s, p);
-        else hipLaunchKernelGGL((memo_search<QSMD_MODEL_TICKET, G64>), dim3(grid), dim3(C_LANES), 0, s, p);
-    } else {
-        if (bank) hipLaunchKernelGGL((memo_search<QSMD_MODEL_BANK, G32>), dim3(grid), dim3(C_LANES), 0, s, p);
-        else hipLaunchKernelGGL((memo_search<QSMD_MODEL_TICKET, G32>), dim3(grid), dim3(C_LANES), 0, s, p);
+}  // namespace
+
+// The heavy stage in lane mode, one launch for both lists: the groups of
+// p32's list (stage 0's heavy histories, <= 32 events) then those of p64's
+// (stage 0w's, <= 64 events), grid-stride.  The LDS (dynamic) holds one
+// group of either geometry when `wide`, else G32 only (14 KB instead of 26:
+// twice the resident wavefronts when the last call had no G64 history in the
+// heavy stage); without it a G64 group goes to the giant stage, which
+// searches any history exactly from the root.
+template <uint32_t MODEL>
+__global__ __launch_bounds__(C_LANES, 3) void memo_search(MemoArgs p32, MemoArgs p64, uint32_t wide) {
+    extern __shared__ uint32_t lds[];
+    const int lane = threadIdx.x;
+    const uint64_t n32 = (*p32.s.list_count + 63u) / 64u, n64 = (*p64.s.list_count + 63u) / 64u;
+    Counters cnt;
+    const uint64_t t0 = p32.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
+    for (uint64_t grp = blockIdx.x; grp < n32 + n64; grp += gridDim.x) {
+        if (grp < n32) {
+            memo_group<MODEL, G32>(p32, grp * 64u, *reinterpret_cast<MemoLds<MODEL, G32>*>(lds), cnt, t0, lane);
+        } else if (wide) {
+            memo_group<MODEL, G64>(p64, (grp - n32) * 64u, *reinterpret_cast<MemoLds<MODEL, G64>*>(lds), cnt, t0,
+                                   lane);
+        } else {
+            const uint64_t idx = (grp - n32) * 64u + lane;
+            const bool in = idx < *p64.s.list_count;
+            wave_append(in, in ? p64.s.list[idx] : 0u, p64.s.giant_list, p64.s.giant_count, lane);
+        }
     }
+    cnt.flush(p32.s.buckets, lane);
+}
+
+hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s) {
+    const bool bank = p32.s.model_id == QSMD_MODEL_BANK;
+    const size_t lds = wide ? (bank ? sizeof(MemoLds<QSMD_MODEL_BANK, G64>) : sizeof(MemoLds<QSMD_MODEL_TICKET, G64>))
+                            : (bank ? sizeof(MemoLds<QSMD_MODEL_BANK, G32>) : sizeof(MemoLds<QSMD_MODEL_TICKET, G32>));
+    if (bank)
+        hipLaunchKernelGGL((memo_search<QSMD_MODEL_BANK>), dim3(grid), dim3(C_LANES), lds, s, p32, p64, wide ? 1u : 0u);
+    else
+        hipLaunchKernelGGL((memo_search<QSMD_MODEL_TICKET>), dim3(grid), dim3(C_LANES), lds, s, p32, p64,
+                           wide ? 1u : 0u);
     return hipGetLastError();
 }
 

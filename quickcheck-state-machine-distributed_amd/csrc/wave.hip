@@ -314,7 +314,7 @@ __device__ void wave_history(const WaveArgs& p, uint32_t h, const qsmd_hdr& H, c
     uint64_t prefix_sum = 0, explored = 0;
     uint32_t best_status = QSMD_STATUS_NONLINEARISABLE, best_depth = 0, work = 0;
     bool incomplete = false, timed = false, skipped = false, overflow = false;
-    uint32_t tick = 0, n_splits = 0, n_hits = 0;
+    uint32_t tick = 0, n_splits = 0;
     const uint64_t c0 = p.stats ? __builtin_amdgcn_s_memtime() : 0;
 
     // record the finished task of every lane with `done` (wave-synchronous)

@@ -229,6 +229,24 @@ def test_heavy_handoff_to_giants(ctx, knobs, split_budget, heavy):
         _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
 
 
+def test_tail_grids_follow_the_previous_call(ctx, knobs):
+    """The tail launches are sized from the previous call's list sizes: a
+    call with no <= 64-event heavy histories, then one with many (lane mode
+    without room for them sends them to the giant stage), then a giant-free
+    call after a giant one -- every result the reference's."""
+    knobs(heavy_mode=1, stage0w_budget=4)
+    for name, first, n in (("bank_4x16", 0, 20000), ("bank_6x24", 3, 5000), ("bank_6x24", 4, 5000),
+                           ("bank_4x16_bugs", 7, 20000)):
+        hdr, ev, _ = gen.generate_config(name, first, n)
+        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+    rng = random.Random(5)
+    hs = [histgen.wellformed_history(rng, "bank", 50, 3, p_pending=0.0) for _ in range(200)]   # 100 events: giants
+    b = codec.encode(models.BANK, hs)
+    _compare(ctx, models.MODEL_BANK, b.hdr, b.events, max_nodes=10**7)
+    hdr, ev, _ = gen.generate_config("bank_4x16", 9, 20000)
+    _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**7)
+
+
 @pytest.mark.parametrize("model", ["ticket", "bank"])
 @pytest.mark.parametrize("heavy", [0, 1])
 def test_heavy_any_shape(ctx, knobs, model, heavy):
