@@ -26,6 +26,11 @@ import os
 import sys
 import time
 
+# HIP reads GPU_MAX_HW_QUEUES when it initialises (the first torch CUDA call):
+# --hw-queues Q sets it for this process before torch is imported
+if "--hw-queues" in sys.argv:
+    os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1]
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "quickcheck-state-machine-distributed_amd")
 sys.path.insert(0, PKG)
@@ -77,7 +82,7 @@ class InFlight:
     the previous call's tail leaves idle).  With RCCL the counters of R rounds
     of steps are all-reduced together, overlapping the next block."""
 
-    def __init__(self, dev, model_id, d_hdr, n, d_ev, n_ev, S, R, flags, use_dist, knobs, budget0):
+    def __init__(self, dev, model_id, d_hdr, n, d_ev, n_ev, S, R, flags, use_dist, knobs, budget0, streams=None):
         self.dev, self.model_id, self.d_hdr, self.n, self.d_ev, self.n_ev = dev, model_id, d_hdr, n, d_ev, n_ev
         self.S, self.B, self.flags = S, R * S, flags
         self.ctxs = [device.Context(dev.index) for _ in range(S)]
@@ -86,7 +91,7 @@ class InFlight:
                 c.set_stage0_budget(budget0)
             for k, v in knobs:
                 c.set_param(k, v)
-        self.streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+        self.streams = streams or [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
         self.outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
                      for _ in range(S)]
         # counters: [block parity][step of the block][8]; a row is reused two blocks later
@@ -272,6 +277,8 @@ def main():
     ap.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
                     help="qsmd_set_param on every context (tuning; repeatable)")
     ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="calls in flight (one context + stream each); 0 = 3 on one GPU, 2 with RCCL "
                          "(its stream takes one of the 4 hardware queues)")
@@ -289,8 +296,26 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or os.environ.get("QSMD_BENCH_DIST") == "1"
+    S = args.inflight if args.inflight > 0 else 3
+    # the slot streams, created and used before RCCL creates its own, so that
+    # each gets a hardware queue of its own (GPU_MAX_HW_QUEUES)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    for st_ in streams:
+        with torch.cuda.stream(st_):
+            torch.ones(1, device=dev).add_(1)
+    torch.cuda.synchronize(dev)
     if use_dist:
-        dist.init_process_group("nccl", device_id=dev)
+        if "RANK" not in os.environ:      # QSMD_BENCH_DIST=1 without a launcher: one rank over RCCL
+            os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=os.environ.get("MASTER_PORT", "29517"))
+        # The RCCL communicator is created lazily, by the warm-up's all-reduce,
+        # after the slot streams and contexts exist: created eagerly at init
+        # (device_id=dev, QSMD_BENCH_EAGER=1) it cost 38 % of one rank's
+        # throughput with no collective issued (profiles/r02/rccl_sweep.txt).
+        if os.environ.get("QSMD_BENCH_EAGER") == "1":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("nccl")
 
     cfg = dict(gen.CONFIGS[args.config])
     model_id = cfg["model_id"]
@@ -312,12 +337,11 @@ def main():
     log(f"[rank {rank}] generated {n} histories ({'device' if args.device_gen else 'host'}) "
         f"in {time.perf_counter() - t:.2f}s")
 
-    S = args.inflight if args.inflight > 0 else (2 if use_dist else 3)
     budget0 = args.stage0_budget if args.stage0_budget is not None else (40 if S > 1 else -1)
     knobs = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in args.param]
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
     run = InFlight(dev, model_id, d_hdr, n, d_ev, len(ev), S, max(1, args.ar_rounds), flags, use_dist, knobs,
-                   budget0)
+                   budget0, streams)
     elapsed = run.timed(args.steps, args.warmup)
     s0_ms, call_ms = run.ctxs[0].timing_read()
     st, nd, tot = run.results()

@@ -1,8 +1,8 @@
 """Fixed per-call cost of the cascade (verdict r01 item 5): device time of a
 call (first event before stage 0 -> event after the giant stage) and host
 wall time per synchronous call, on tiny batches of config 2 with the default
-parameters.  One call is 5 launches (stage 0, stage 0w, heavy G32, heavy
-G64, giant stage); with nothing to do, the last four return at once.
+parameters.  One call is 4 launches (stage 0, stage 0w, the heavy stage,
+the giant stage); with nothing to do, the last three return at once.
 
     python tools/overhead.py [--calls 300] [--param NAME=VALUE ...]
 Prints one JSON line per batch size.
@@ -61,7 +61,7 @@ def main():
             torch.cuda.synchronize()
             walls.append(time.perf_counter() - t)
         ok = bool((d_st.cpu().numpy() == 1).all())
-        print(json.dumps({"n_hist": n, "launches_per_call": 5,
+        print(json.dumps({"n_hist": n, "launches_per_call": 4,
                           "device_us_median": round(1e3 * float(np.median(dev_ms)), 2),
                           "stage0_us_median": round(1e3 * float(np.median(s0)), 2),
                           "sync_wall_us_median": round(1e6 * float(np.median(walls)), 2),
