@@ -7,11 +7,13 @@
 //                                  a node budget          (csrc/compact.hip)
 //   stage 0w  compact_search<G64>  the histories stage 0 cannot hold, <= 64
 //                                  events                 (csrc/compact.hip)
-//   heavy     wave_search          the histories over the stage-0 / 0w
-//                                  budgets, one wavefront per history with a
-//                                  shared LDS state memo  (csrc/wave.hip), or
-//                                  memo_search (one per lane, HBM memo) when
-//                                  such histories are many (csrc/memo.hip)
+//   heavy     memo_search          the histories over the stage-0 / 0w
+//                                  budgets (both lists, one launch), one per
+//                                  lane with an exact-count HBM memo
+//                                  (csrc/memo.hip; heavy_mode 1, default), or
+//                                  wave_search, one wavefront per history
+//                                  with an LDS memo (csrc/wave.hip; heavy_mode
+//                                  0, or 2 = by the last call's count)
 //   giants    giant_search         everything else: the split stage (one
 //                                  history over many lanes), the ordered
 //                                  combine, the batch totals (csrc/split.hip)

@@ -1,9 +1,10 @@
 // lane.h -- the per-lane search machinery shared by the compact-domain
-// kernels (csrc/compact.hip: stage 0 and the refill stage; csrc/spread.hip:
-// the dynamic split stage): the compressed event format, the staging paths,
-// and LaneDFS, the reference DFS (src/Linearisability.hs:25-69 over the
-// Lemma L1 event bitset) as a per-lane state machine for histories of at
-// most 32 events and 8 pids.
+// kernels (csrc/compact.hip: stages 0 and 0w; csrc/memo.hip: the heavy
+// stage in lane mode; csrc/wave.hip: the heavy stage in wave mode): the
+// compressed event format, the staging paths, and LaneDFS, the reference
+// DFS (src/Linearisability.hs:25-69 over the Lemma L1 event bitset) as a
+// per-lane state machine for histories of at most 32 (G32) or 64 (G64)
+// events and 8 pids.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -28,7 +29,7 @@ constexpr int32_t V19_MIN = -(1 << 18), V19_MAX = (1 << 18) - 1;   // model0 val
 // index of the response paired with the invocation (0 = none: pending).
 // Staging writes a marker instead of an event it cannot hold: an invocation
 // with code 7 (not an encodable event: ENCODE_ERROR) or code 6 (a value
-// outside the ranges above: the history goes to stage 1).
+// outside the ranges above: the history goes to the next stage).
 constexpr int32_t IVAL_BITS = 14, RVAL_BITS = 25;
 constexpr uint32_t MARK_BAD = 0x70u, MARK_WIDE = 0x60u;
 // Geometry of a compact stage: <= 32 events (u32 event masks, 16 levels,
@@ -360,7 +361,7 @@ __device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane,
     s.paired = unpaired == 0u;
 }
 
-// finish_lane for a history shared by the wavefront (csrc/coop.hip): every
+// finish_lane for a history shared by the wavefront (csrc/wave.hip): every
 // lane derives the same masks from s_hist[e]; only `writer` ORs the pairs in.
 template <class G = G32>
 __device__ __forceinline__ void finish_shared(uint32_t* s_hist, bool writer, uint32_t n_ev, uint32_t n_pid,

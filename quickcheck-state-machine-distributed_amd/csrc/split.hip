@@ -99,8 +99,8 @@ struct Memo {
     // epoch24 << 40 | (giant + 1) << 8 | hash7 << 1 | ready.  Writers claim an
     // empty or stale (older epoch) slot by CAS, store key and count with
     // agent-scope (sc1) stores, drain them, then set the ready bit; readers use
-    // sc1 loads (the protocol of the QSMD_FLAG_MEMO table and the spread
-    // stage's task records) and take a count only under a ready, matching tag
+    // sc1 loads (the protocol of the QSMD_FLAG_MEMO table) and take a count
+    // only under a ready, matching tag
     // and all seven key words.
     __device__ uint64_t xtag(const MemoKey& k, uint32_t id) const {
         return ((uint64_t)(epoch & 0xFFFFFFu) << 40) | ((uint64_t)(id + 1u) << 8) | ((k.hash >> 56) & 0xFEull);

@@ -2,7 +2,7 @@
 advancedtelematic/quickcheck-state-machine-distributed (src/Linearisability.hs).
 
 Host-side mirror of the reference interface; the search runs in hand-written
-HIP kernels (csrc/search.hip) behind the C ABI of include/qsmd.h.
+HIP kernels (csrc/*.hip, lib/libqsmd.so) behind the C ABI of include/qsmd.h.
 """
 
 from .codec import Left, Right, encode, decode_history, STATUS_NAMES  # noqa: F401
