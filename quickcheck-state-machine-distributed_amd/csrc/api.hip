@@ -70,7 +70,7 @@ struct qsmd_ctx {
     uint32_t* probe_host = nullptr;    // pinned: [defer, heavy32, heavy64, giant] of the last finished call
     uint32_t* debug_host = nullptr;    // QSMD_SYNC_STAGES: giant-stage heartbeat (pinned)
     // lane mode's tables: one per lane slot of the memo grid
-    uint64_t memo_grid = 2048;
+    uint64_t memo_grid = 4096;         // heavy stage (lane mode): workgroups at most; one private table each
     uint64_t mt_entries = 256;
     char* mt = nullptr;
     size_t mt_bytes = 0;

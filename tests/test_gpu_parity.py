@@ -96,7 +96,7 @@ def test_random_any_shape(ctx, model):
 
 
 DEFAULTS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 1, "wave_budget": 16, "wave_max": 16384,
-            "split_budget": 1024, "memo_lane_entries": 256, "memo_grid": 2048, "split_xmemo": 1}
+            "split_budget": 1024, "memo_lane_entries": 256, "memo_grid": 4096, "split_xmemo": 1}
 
 
 @pytest.fixture
