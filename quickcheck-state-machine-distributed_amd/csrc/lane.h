@@ -559,7 +559,9 @@ struct LaneDFS {
             const uint32_t exp = __builtin_amdgcn_ubfe(kBankExp2, code * 6u + sel * 3u, 3u);
             const bool inv_ok = neg == 0u;
             err = has & inv_ok & chk & (rc == QSMD_BANK_BALANCE) & !ex_a;   // Map.! raises
-            ok = has & !over & inv_ok & (rc == exp) & (!chk | (rv == bal_a));
+            // a raising step never descends (an absent account's stored 0
+            // would otherwise match `Balance 0`)
+            ok = has & !over & inv_ok & !err & (rc == exp) & (!chk | (rv == bal_a));
             // next' (test/Bank.hs:92-101) on a (an absent account is created
             // with m exactly when the step's sign is non-zero: insertWith),
             // then Transfer's deposit on b; stored unconditionally (the old

@@ -143,7 +143,7 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     if (d.cand) {
         const uint32_t dep0 = d.depth;
         status = d.template try_next<C_LANES, MODE>(a, evc, s_bal, lane, limit);
-        if (d.depth > dep0) {                     // entered a new node
+        if (d.depth > dep0 && status < 0) {       // entered a new node (and the search goes on)
             entry[dep0 * C_LANES] = (uint32_t)d.nodes;
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             uint32_t cnt = 0;

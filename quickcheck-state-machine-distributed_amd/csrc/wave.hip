@@ -275,7 +275,8 @@ __device__ __forceinline__ int wave_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     if (d.cand) {
         const uint32_t dep0 = d.depth;
         status = d.template try_next<1, MODE>(a, hist, s_bal, lane, limit);
-        if (d.depth > dep0 && (uint32_t)__builtin_popcountll((uint64_t)d.rem) > min_rem) {   // entered a new node
+        if (d.depth > dep0 && status < 0 &&
+            (uint32_t)__builtin_popcountll((uint64_t)d.rem) > min_rem) {   // entered a new node (the search goes on)
             entry[dep0 * C_LANES] = (uint32_t)d.nodes;
             const WKey k = wave_key<MODEL, G>(d, a, s_bal, lane);
             uint32_t c = 0;

@@ -229,6 +229,21 @@ def test_heavy_handoff_to_giants(ctx, knobs, split_budget, heavy):
         _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
 
 
+@pytest.mark.parametrize("heavy,w_budget,split", [(0, 4, 64), (1, 4, 64), (0, 1, 1024), (1, 1, 1024),
+                                                  (0, 0, 1024), (0, 4, 1)])
+def test_model_error_in_the_heavy_stage(ctx, knobs, heavy, w_budget, split):
+    """A 33-event unpaired Bank history that ends in Map.! after 7 nodes
+    (found by tools/stress_parity.py --seed 11 --knobs, batch 219), through
+    stage 0w's budget into both heavy-stage modes: the count stops at the
+    raising node."""
+    import os
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "wave_model_error_case.npz"))
+    hdr, ev, mid = f["hdr"], f["ev"], int(f["model_id"])
+    knobs(heavy_mode=heavy, stage0_budget=4, stage0w_budget=w_budget, split_budget=split)
+    st, nd, _ = _compare(ctx, mid, np.repeat(hdr, 3), ev, max_nodes=200000)
+    assert (st == int(f["status"])).all() and (nd == int(f["nodes"])).all()
+
+
 def test_tail_grids_follow_the_previous_call(ctx, knobs):
     """The tail launches are sized from the previous call's list sizes: a
     call with no <= 64-event heavy histories, then one with many (lane mode

@@ -1,8 +1,9 @@
 """Randomised parity sweep (test infrastructure): generated batches with
 random generator parameters and random any-shape histories, through the
-default cascade (adaptive probe, memo stage, witnesses), against the C
-oracle.  Prints one JSON summary line; exits 1 on any mismatch.
-    python tools/stress_parity.py [--batches 40] [--seed 1]"""
+cascade with witnesses and, per batch, random stage budgets and heavy-stage
+mode (--knobs; the default cascade otherwise), against the C oracle.
+Prints one JSON summary line; exits 1 on any mismatch.
+    python tools/stress_parity.py [--batches 40] [--seed 1] [--knobs]"""
 
 import argparse
 import json
@@ -26,6 +27,9 @@ from qsmd import codec, device, gen, models  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--batches", type=int, default=40)
 ap.add_argument("--seed", type=int, default=1)
+ap.add_argument("--knobs", action="store_true", help="random stage budgets / heavy mode per batch")
+ap.add_argument("--only", type=int, default=-1, help="check only this batch (the others only draw their randoms)")
+ap.add_argument("--dump", default="gpurun_out/stress_mismatch", help="mismatching batches: <dump>_<batch>.npz")
 args = ap.parse_args()
 rng = random.Random(args.seed)
 ctx = device.Context(0, time_limit_ms=60000)
@@ -34,9 +38,17 @@ stats = {"batches": 0, "histories": 0, "nodes": 0, "mismatch_status": 0, "mismat
          "mismatch_witness": 0, "lin": 0, "nonlin": 0, "error": 0, "encode": 0}
 
 
-def compare(model_id, hdr, ev, model0=None):
+def compare(model_id, hdr, ev, model0=None, batch=-1, knobs=None):
     st_d, nd_d, w_d, _ = ctx.check_arrays(model_id, hdr, ev, model0, max_nodes=200_000, witness=True)
     st_o, nd_o, w_o = oracle_c.check_batch(model_id, hdr, ev, model0, 200_000, 16, witness=True)
+    bad = np.nonzero((st_d != st_o) | (nd_d != nd_o))[0]
+    if len(bad):
+        os.makedirs(os.path.dirname(args.dump) or ".", exist_ok=True)
+        np.savez(f"{args.dump}_{batch}.npz", hdr=hdr, ev=ev, bad=bad, model_id=model_id,
+                 knobs=json.dumps(knobs or {}), st_d=st_d[bad], nd_d=nd_d[bad], st_o=st_o[bad], nd_o=nd_o[bad])
+        print(json.dumps({"batch": batch, "knobs": knobs, "bad": bad[:8].tolist(), "dev": [st_d[bad[:8]].tolist(),
+                          nd_d[bad[:8]].tolist()], "oracle": [st_o[bad[:8]].tolist(), nd_o[bad[:8]].tolist()]}),
+              file=sys.stderr, flush=True)
     stats["batches"] += 1
     stats["histories"] += len(hdr)
     stats["nodes"] += int(nd_o.sum())
@@ -49,7 +61,15 @@ def compare(model_id, hdr, ev, model0=None):
         stats[k] += int((st_o == s).sum())
 
 
+KNOBS = {"stage0_budget": [0, 4, 16, 32, 40, 64], "stage0w_budget": [0, 4, 32], "heavy_mode": [0, 1, 2],
+         "split_budget": [64, 1024]}
 for b in range(args.batches):
+    knobs = {}
+    if args.knobs:
+        for k, vals in KNOBS.items():
+            knobs[k] = rng.choice(vals)
+            ctx.set_param(k, knobs[k])
+    check = args.only < 0 or args.only == b
     if b % 2 == 0:                               # generator with random parameters
         name = rng.choice(list(gen.CONFIGS))
         kw = dict(gen.CONFIGS[name])
@@ -62,8 +82,10 @@ for b in range(args.batches):
         kw["lin_policy"] = rng.randint(0, 1)
         kw["money_max"] = rng.choice([3, 10, 100])
         kw["seed"] = rng.getrandbits(48)
-        hdr, ev, _ = gen.generate(gen.params(**kw), rng.randint(0, 10**6), 20000 if kw["n_ops"] <= 32 else 4000)
-        compare(kw["model_id"], hdr, ev)
+        first = rng.randint(0, 10**6)
+        if check:
+            hdr, ev, _ = gen.generate(gen.params(**kw), first, 20000 if kw["n_ops"] <= 32 else 4000)
+            compare(kw["model_id"], hdr, ev, batch=b, knobs=knobs)
     else:                                        # any shape (ill-formed, shared pids, pending, errors)
         model = rng.choice(["ticket", "bank"])
         hs = []
@@ -73,8 +95,11 @@ for b in range(args.batches):
             else:
                 hs.append(histgen.wellformed_history(rng, model, rng.randint(1, 24), rng.randint(1, 8)))
         m = models.BY_NAME[model]
-        bt = codec.encode(m, hs)
-        compare(m.model_id, bt.hdr, bt.events)
+        if check:
+            bt = codec.encode(m, hs)
+            compare(m.model_id, bt.hdr, bt.events, batch=b, knobs=knobs)
+    if not check:
+        continue
     print(json.dumps({"batch": b, **{k: stats[k] for k in ("histories", "mismatch_status", "mismatch_nodes",
                                                            "mismatch_witness")},
                       "t": round(time.time() - t0, 1)}), file=sys.stderr, flush=True)
