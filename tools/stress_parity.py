@@ -3,7 +3,7 @@ random generator parameters and random any-shape histories, through the
 cascade with witnesses and, per batch, random stage budgets and heavy-stage
 mode (--knobs; the default cascade otherwise), against the C oracle.
 Prints one JSON summary line; exits 1 on any mismatch.
-    python tools/stress_parity.py [--batches 40] [--seed 1] [--knobs]"""
+    python tools/stress_parity.py [--batches 40] [--seed 1] [--knobs] [--wide]"""
 
 import argparse
 import json
@@ -28,6 +28,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--batches", type=int, default=40)
 ap.add_argument("--seed", type=int, default=1)
 ap.add_argument("--knobs", action="store_true", help="random stage budgets / heavy mode per batch")
+ap.add_argument("--wide", action="store_true", help="also any-shape histories up to 100 events / 12 pids")
 ap.add_argument("--only", type=int, default=-1, help="check only this batch (the others only draw their randoms)")
 ap.add_argument("--dump", default="gpurun_out/stress_mismatch", help="mismatching batches: <dump>_<batch>.npz")
 args = ap.parse_args()
@@ -62,7 +63,8 @@ def compare(model_id, hdr, ev, model0=None, batch=-1, knobs=None):
 
 
 KNOBS = {"stage0_budget": [0, 4, 16, 32, 40, 64], "stage0w_budget": [0, 4, 32], "heavy_mode": [0, 1, 2],
-         "split_budget": [64, 1024]}
+         "split_budget": [1, 16, 64, 1024], "memo_lane_entries": [2, 256], "wave_budget": [1, 16],
+         "wave_min_rem": [0, 8], "split_xmemo": [0, 1]}
 for b in range(args.batches):
     knobs = {}
     if args.knobs:
@@ -89,11 +91,14 @@ for b in range(args.batches):
     else:                                        # any shape (ill-formed, shared pids, pending, errors)
         model = rng.choice(["ticket", "bank"])
         hs = []
-        for _ in range(3000):
+        wide = args.wide and rng.random() < 0.3      # beyond the compact stages: the giant stage
+        for _ in range(1000 if wide else 3000):
             if rng.random() < 0.5:
-                hs.append(histgen.random_history(rng, model, rng.randint(0, 40), rng.randint(1, 8)))
+                hs.append(histgen.random_history(rng, model, rng.randint(0, 100 if wide else 40),
+                                                 rng.randint(1, 12 if wide else 8)))
             else:
-                hs.append(histgen.wellformed_history(rng, model, rng.randint(1, 24), rng.randint(1, 8)))
+                hs.append(histgen.wellformed_history(rng, model, rng.randint(1, 50 if wide else 24),
+                                                     rng.randint(1, 12 if wide else 8)))
         m = models.BY_NAME[model]
         if check:
             bt = codec.encode(m, hs)
