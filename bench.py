@@ -293,6 +293,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # QSMD_BENCH_DEVICE / QSMD_BENCH_BACKEND=gloo: a multi-rank rehearsal on
+    # one GPU (RCCL refuses two ranks on one device); diagnostics only
+    if os.environ.get("QSMD_BENCH_DEVICE"):
+        local = int(os.environ["QSMD_BENCH_DEVICE"])
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or os.environ.get("QSMD_BENCH_DIST") == "1"
@@ -312,7 +316,9 @@ def main():
         # after the slot streams and contexts exist: created eagerly at init
         # (device_id=dev, QSMD_BENCH_EAGER=1) it cost 38 % of one rank's
         # throughput with no collective issued (profiles/r02/rccl_sweep.txt).
-        if os.environ.get("QSMD_BENCH_EAGER") == "1":
+        if os.environ.get("QSMD_BENCH_BACKEND") == "gloo":
+            dist.init_process_group("gloo")
+        elif os.environ.get("QSMD_BENCH_EAGER") == "1":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("nccl")
