@@ -206,8 +206,8 @@ int qsmd_set_stage0_grid(qsmd_ctx* ctx, uint64_t max_blocks);
 
 /* Tuning knob: node budget of the first search stage (default 32; 0 = none).
  * A history whose search needs more nodes is searched again, from the root,
- * by the heavy stage (one wavefront per history), so one long search does
- * not hold 63 idle lanes.  Results are unchanged. */
+ * by the heavy stage (one lane per history with an exact-count state memo),
+ * so one long search does not hold 63 idle lanes.  Results are unchanged. */
 int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
 
 /* Tuning knobs by name (none changes a result):
@@ -216,16 +216,29 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *   "stage0_grid"       as qsmd_set_stage0_grid
  *   "split_budget"      as qsmd_set_split_budget
  *   "split_xmemo"       1 (default): the giant stage's exact-count memo
- *   "wave_budget"       heavy stage: nodes a lane's task counts before it
- *                       may hand the rest to idle lanes (default 16)
- *   "wave_grid"         heavy stage workgroups (0 = 3 per CU)
- *   "giant_grid"        giant stage workgroups (0 = 2 per CU)
- *   "heavy_mode"        0: one wavefront per heavy history; 1: one lane per
- *                       heavy history with a private HBM memo table; 2
- *                       (default): lane mode while the last finished call
+ *   "heavy_mode"        1 (default): one lane per heavy history with a
+ *                       private memo table; 0: one wavefront per heavy
+ *                       history; 2: lane mode while the last finished call
  *                       sent more than "wave_max" (default 16384) histories
- *                       to the heavy stage
- *   "memo_grid", "memo_lane_entries"  lane mode: workgroups, entries per lane */
+ *                       to the heavy stage, else wave mode
+ *   "memo_lds"          lane mode's memo tables: 1 (default) in LDS when the
+ *                       last finished call's heavy histories fit one
+ *                       workgroup per CU (fastest for one call at a time),
+ *                       else in HBM; 0: always HBM (better with several
+ *                       calls in flight: an LDS-table workgroup holds a CU);
+ *                       2: always LDS
+ *   "memo_grid", "memo_lane_entries"  lane mode: workgroups, entries per lane
+ *                       (HBM; the LDS tables hold min(64, entries))
+ *   "wave_budget"       wave mode: nodes a lane's task counts before it may
+ *                       hand the rest to idle lanes (default 16)
+ *   "wave_grid"         wave mode workgroups (0 = 3 per CU)
+ *   "wave_min_rem"      wave mode: no memo probe below this many remaining
+ *                       events
+ *   "giant_grid"        giant stage workgroups (0 = 2 per CU, or 64 when the
+ *                       last finished call had no giant history)
+ *   "wave_stats_ptr", "memo_stats_ptr", "memo_stats_groups"  diagnostics:
+ *                       device buffers of per-workgroup / per-group records
+ *                       (tools/wave_stats.py, tools/memo_stats.py) */
 int qsmd_set_param(qsmd_ctx* ctx, const char* name, uint64_t value);
 
 /* Tuning knob (default 1024): histories the compact stages cannot hold go to

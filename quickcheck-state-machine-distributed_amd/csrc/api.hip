@@ -60,6 +60,9 @@ struct qsmd_ctx {
     uint64_t wave_grid = 0;            // heavy stage workgroups (0 = 3 per CU)
     uint64_t wave_min_rem = 8;         // heavy stage: nodes with at most this many events left skip the memo
     unsigned long long* wave_stats = nullptr;   // diagnostic (wave_stats_ptr): 8 x u64 per workgroup
+    unsigned long long* memo_stats = nullptr;   // diagnostic (memo_stats_ptr): 8 x u64 per heavy-stage group
+    uint64_t memo_stats_groups = 0;             // (memo_stats_groups)
+    uint32_t memo_lds = 1;                      // heavy-stage memo tables in LDS: 0 never, 1 short lists, 2 always
     uint64_t giant_grid = 0;           // giant stage workgroups (0 = 2 per CU)
     // heavy stage: one wavefront per history (wave_search) unless the last
     // finished call sent more than wave_max histories there (then one lane
@@ -298,6 +301,13 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->wave_min_rem = std::min<uint64_t>(value, 0xFFFFFFFFull);
     } else if (n == "wave_stats_ptr") {     // diagnostic: device buffer of 8 x u64 per wave_search workgroup
         c->wave_stats = reinterpret_cast<unsigned long long*>(value);
+    } else if (n == "memo_stats_ptr") {     // diagnostic: device buffer of 8 x u64 per heavy-stage group (zeroed)
+        c->memo_stats = reinterpret_cast<unsigned long long*>(value);
+    } else if (n == "memo_stats_groups") {
+        c->memo_stats_groups = value;
+    } else if (n == "memo_lds") {
+        if (value > 2) return fail(c, QSMD_ERR_ARG, "memo_lds: 0 = HBM tables, 1 = LDS for short lists, 2 = LDS");
+        c->memo_lds = (uint32_t)value;
     } else if (n == "heavy_mode") {
         if (value > 2) return fail(c, QSMD_ERR_ARG, "heavy_mode: 0 = wave, 1 = lane, 2 = auto");
         c->heavy_mode = value;
@@ -523,11 +533,21 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].entries = (uint32_t)c->mt_entries;
             mp[w].epoch = c->mt_epoch;
             mp[w].giant_cap = cap;
+            mp[w].stats = c->memo_stats;
+            mp[w].stats_groups = c->memo_stats ? c->memo_stats_groups : 0;
         }
         // G64 groups in this launch only when the last call had some (else they go to the giant stage)
         const bool wide = hint[2] != 0u;
-        HIP_TRY(c, launch_memo(mp[0], mp[1], (uint32_t)tail_grid(c, c->memo_grid, (uint64_t)hint[1] + hint[2]), wide, s),
-                "memo launch");
+        // the memo tables in LDS (one wavefront per CU) when the last call's
+        // heavy groups fit the CUs: the stage is then one search's latency
+        const uint64_t g32 = c->probe_valid ? ((uint64_t)hint[1] + 63u) / 64u : ~0ull;
+        const bool lt = c->memo_lds == 2 || (c->memo_lds == 1 && g32 <= (uint64_t)c->n_cu);
+        // (LDS tables: one workgroup per CU, so no idle workgroups beyond
+        // twice the groups expected -- they would hold CUs the next call's
+        // stage 0 could use)
+        const uint64_t mg = lt && !wide ? std::min<uint64_t>(c->n_cu, 2 * std::min<uint64_t>(g32, c->n_cu) + 8)
+                                        : tail_grid(c, c->memo_grid, (uint64_t)hint[1] + hint[2]);
+        HIP_TRY(c, launch_memo(mp[0], mp[1], (uint32_t)mg, wide, lt, s), "memo launch");
         stage_done("lane", s, cnt);
     } else {
         WaveArgs wp{};

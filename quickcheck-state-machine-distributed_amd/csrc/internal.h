@@ -228,8 +228,12 @@ struct MemoArgs {
     uint32_t entries;
     uint32_t epoch;               // this call's tag (24 bits)
     uint64_t giant_cap;           // > 0: a search past this many iterations goes to s.giant_list
+    unsigned long long* stats;    // diagnostic (memo_stats_ptr): 8 x u64 per group of the launch, or null
+    uint64_t stats_groups;        // groups the stats buffer holds
 };
-hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s);
+// lds_tables: the G32 memo tables in LDS (ignored with `wide`)
+hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool lds_tables,
+                       hipStream_t s);
 
 hipError_t launch_gen(const qsmd_gen_params& p, uint64_t first, uint64_t n_hist, uint32_t ev_base, qsmd_hdr* hdr,
                       qsmd_event* events, uint8_t* bug_out, hipStream_t s);

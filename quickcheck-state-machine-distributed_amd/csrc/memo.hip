@@ -50,15 +50,6 @@ struct MemoKey {
     bool ok;
 };
 
-__device__ __forceinline__ uint32_t mix32(uint32_t h) {
-    h ^= h >> 16;
-    h *= 0x7FEB352Du;
-    h ^= h >> 15;
-    h *= 0x846CA68Bu;
-    h ^= h >> 16;
-    return h;
-}
-
 // the key of the lane's current state (the node at depth dfs.depth)
 template <uint32_t MODEL, class G>
 __device__ __forceinline__ MemoKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d, const SearchArgs& a,
@@ -71,10 +62,12 @@ __device__ __forceinline__ MemoKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d
     uint32_t ex = 0;
     if constexpr (MODEL == QSMD_MODEL_BANK) {
         ex = d.ex;
+        // an absent account holds 0 in LDS (LaneDFS: created from 0, restored
+        // to 0 by undo), so the balances are read unconditionally
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int32_t b0 = ((ex >> (2 * q)) & 1u) ? s_bal[2 * q][lane] : 0;
-            const int32_t b1 = ((ex >> (2 * q + 1)) & 1u) ? s_bal[2 * q + 1][lane] : 0;
+            const int32_t b0 = s_bal[2 * q][lane];
+            const int32_t b1 = s_bal[2 * q + 1][lane];
             k.ok = k.ok && b0 == (int32_t)(int16_t)b0 && b1 == (int32_t)(int16_t)b1;
             k.m[q] = ((uint32_t)b0 & 0xFFFFu) | ((uint32_t)b1 << 16);
         }
@@ -88,10 +81,12 @@ __device__ __forceinline__ MemoKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d
         k.m[1] = k.m[2] = k.m[3] = 0u;
     }
     k.w1 = (epoch & 0xFFFFFFu) | (ex << 24);
-    uint32_t h = mix32(k.rem_lo ^ 0x9E3779B9u);
-    h = mix32(h ^ k.rem_hi ^ (k.w1 >> 24));
-#pragma unroll
-    for (int q = 0; q < 4; ++q) h = mix32(h ^ k.m[q]);
+    // slot: three independent multiplicative hashes, folded (a short
+    // dependent chain: the key is computed twice per DFS iteration)
+    const uint32_t v = (k.m[0] ^ __builtin_amdgcn_alignbit(k.m[1], k.m[1], 8)) ^
+                       (__builtin_amdgcn_alignbit(k.m[2], k.m[2], 16) ^ __builtin_amdgcn_alignbit(k.m[3], k.m[3], 24));
+    uint32_t h = (k.rem_lo * 0x9E3779B1u) ^ ((k.rem_hi ^ ex) * 0x85EBCA77u) ^ (v * 0xC2B2AE3Du);
+    h ^= (h >> 16) ^ (h >> 24);   // the low bits see every input bit through the products' top bits
     k.slot = h & mask;
     return k;
 }
@@ -116,9 +111,44 @@ __device__ __forceinline__ void memo_insert(uint32_t* tab, const MemoKey<MODEL, 
     if constexpr (G::EV == 64) e[2] = make_uint4(k.rem_hi, 0u, 0u, 0u);
 }
 
+// The LDS table (G32, a short heavy list): kLdsEntries direct-mapped entries
+// per lane, word w of entry e at col[(e * 8 + w) * 64] (each lane its own
+// bank); an LDS probe instead of an HBM round trip per node.  128 KB per
+// workgroup: one wavefront per CU, chosen only when the heavy groups fit
+// the CUs (api.hip).  Word 0 holds the history index; kNoHistory = empty.
+constexpr uint32_t kLdsEntries = 64;
+constexpr uint32_t kNoHistory = 0xFFFFFFFFu;
+
+template <uint32_t MODEL, class G>
+__device__ __forceinline__ bool memo_lookup_lds(const uint32_t* col, const MemoKey<MODEL, G>& k, uint32_t h,
+                                                uint32_t& count) {
+    const uint32_t* e = col + k.slot * 8u * C_LANES;
+    bool hit = e[0] == h && e[1 * C_LANES] == k.w1 && e[2 * C_LANES] == k.rem_lo && e[4 * C_LANES] == k.m[0];
+    if constexpr (MODEL == QSMD_MODEL_BANK)
+        hit = hit && e[5 * C_LANES] == k.m[1] && e[6 * C_LANES] == k.m[2] && e[7 * C_LANES] == k.m[3];
+    count = e[3 * C_LANES];
+    return hit;
+}
+
+template <uint32_t MODEL, class G>
+__device__ __forceinline__ void memo_insert_lds(uint32_t* col, const MemoKey<MODEL, G>& k, uint32_t h, uint32_t count) {
+    uint32_t* e = col + k.slot * 8u * C_LANES;
+    e[0] = h;
+    e[1 * C_LANES] = k.w1;
+    e[2 * C_LANES] = k.rem_lo;
+    e[3 * C_LANES] = count;
+    e[4 * C_LANES] = k.m[0];
+    if constexpr (MODEL == QSMD_MODEL_BANK) {
+        e[5 * C_LANES] = k.m[1];
+        e[6 * C_LANES] = k.m[2];
+        e[7 * C_LANES] = k.m[3];
+    }
+}
+
 // One DFS iteration with the memo (LaneDFS::step plus the two hooks).
-// entry: the lane's column of node counts at entry, per level.
-template <uint32_t MODEL, class G, int MODE>
+// entry: the lane's column of node counts at entry, per level; tab: the
+// lane's HBM table, or (LT) its LDS column.
+template <uint32_t MODEL, class G, int MODE, bool LT>
 __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* evc,
                                          int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* tab,
                                          uint32_t h, uint32_t epoch, uint32_t mask, uint32_t* entry, bool& skip) {
@@ -133,7 +163,10 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
         if (!skip && d.nodes <= 0xFFFFFFFFull) {
             const uint32_t cnt = (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES];
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
-            if (k.ok) memo_insert<MODEL, G>(tab, k, h, cnt);
+            if (k.ok) {
+                if constexpr (LT) memo_insert_lds<MODEL, G>(tab, k, h, cnt);
+                else memo_insert<MODEL, G>(tab, k, h, cnt);
+            }
         }
         skip = false;
         const uint32_t j = d.template undo<C_LANES, MODE>(evc, s_bal, lane);
@@ -147,7 +180,12 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
             entry[dep0 * C_LANES] = (uint32_t)d.nodes;
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             uint32_t cnt = 0;
-            if (k.ok && memo_lookup<MODEL, G>(tab, k, h, cnt)) {
+            bool hit = false;
+            if (k.ok) {
+                if constexpr (LT) hit = memo_lookup_lds<MODEL, G>(tab, k, h, cnt);
+                else hit = memo_lookup<MODEL, G>(tab, k, h, cnt);
+            }
+            if (hit) {
                 if (d.nodes + cnt > limit) {      // the budget falls inside that subtree
                     d.nodes = limit;
                     status = QSMD_STATUS_BUDGET;
@@ -176,18 +214,31 @@ struct MemoLds {
 
 // One group of 64 histories of p's list (from index base); every history of
 // the list fits geometry G (a compact stage staged it before).
-template <uint32_t MODEL, class G>
-__device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, MemoLds<MODEL, G>& L, Counters& cnt,
-                                           uint64_t t0, int lane) {
+// ST: diagnostic build of the loop, one record per group in p.stats
+// (realtime at start / staged / end, max and summed DFS iterations over the
+// lanes, memo hits, histories, shader cycles of the search loop).
+template <uint32_t MODEL, class G, bool LT, bool ST>
+__device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, MemoLds<MODEL, G>& L, uint32_t* lcol,
+                                           Counters& cnt, uint64_t t0, int lane, unsigned long long* q) {
     using M = typename G::M;
     const SearchArgs& a = p.s;
     const uint64_t total = *a.list_count;
     const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
-    uint32_t* tab = p.table + ((uint64_t)blockIdx.x * C_LANES + (uint64_t)lane) * (uint64_t)p.entries *
-                                  (uint64_t)MemoEntry<G>::W;
-    const uint32_t mask = p.entries - 1u;
+    uint32_t* tab;
+    uint32_t mask;
+    if constexpr (LT) {
+        tab = lcol;
+        mask = (p.entries < kLdsEntries ? p.entries : kLdsEntries) - 1u;
+    } else {
+        tab = p.table + ((uint64_t)blockIdx.x * C_LANES + (uint64_t)lane) * (uint64_t)p.entries *
+                            (uint64_t)MemoEntry<G>::W;
+        mask = p.entries - 1u;
+    }
     const uint64_t idx = base + lane;
     const bool active = idx < total;
+    uint64_t r0 = 0, c0 = 0;
+    uint32_t hits = 0;
+    if constexpr (ST) r0 = __builtin_amdgcn_s_memrealtime();
     const uint32_t h = active ? a.list[idx] : 0u;
     qsmd_hdr H;
     if (active) H = a.hdr[h];
@@ -196,6 +247,13 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
     if (active) {
         stage_lane<MODEL, G>(a, H, L.ev, lane);
         finish_lane<G>(L.ev, lane, H.n_ev, H.n_pid, s);
+    }
+    if constexpr (ST) {
+        c0 = __builtin_amdgcn_s_memtime();
+        if (lane == 0) {
+            q[0] = r0;
+            q[1] = __builtin_amdgcn_s_memrealtime();
+        }
     }
     if (!active) return;
     int status = -1;
@@ -217,8 +275,10 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
         bool skip = false;
         uint32_t iter = 0;
         do {
-            status = memo_step<MODEL, G, M_LANE>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch, mask,
+            const bool was = skip;
+            status = memo_step<MODEL, G, M_LANE, LT>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch, mask,
                                                  &L.entry[0][lane], skip);
+            if constexpr (ST) hits += (!was && skip) ? 1u : 0u;
             ++iter;
             if (p.giant_cap && iter >= p.giant_cap && status < 0) {
                 status = QSMD_STATUS_HANDED_OFF;
@@ -231,6 +291,16 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
                 }
             }
         } while (status < 0);
+        if constexpr (ST) {
+            atomicMax(q + 3, (unsigned long long)iter);
+            atomicAdd(q + 4, (unsigned long long)iter);
+            atomicAdd(q + 5, (unsigned long long)hits);
+            atomicMax(q + 7, (unsigned long long)(__builtin_amdgcn_s_memtime() - c0));
+        }
+    }
+    if constexpr (ST) {
+        atomicAdd(q + 6, 1ull);
+        atomicMax(q + 2, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
     if (status == QSMD_STATUS_HANDED_OFF) {      // the giant stage searches it (exact, from the root)
         a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
@@ -251,20 +321,31 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
 // group of either geometry when `wide`, else G32 only (14 KB instead of 26:
 // twice the resident wavefronts when the last call had no G64 history in the
 // heavy stage); without it a G64 group goes to the giant stage, which
-// searches any history exactly from the root.
-template <uint32_t MODEL>
-__global__ __launch_bounds__(C_LANES, 3) void memo_search(MemoArgs p32, MemoArgs p64, uint32_t wide) {
+// searches any history exactly from the root.  LT (never with `wide`): the
+// G32 memo tables in LDS after the group (a short list: the heavy stage's
+// time is one search's DFS chain, and the HBM probe was half of it).
+template <uint32_t MODEL, bool LT>
+__global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32, MemoArgs p64, uint32_t wide) {
     extern __shared__ uint32_t lds[];
     const int lane = threadIdx.x;
     const uint64_t n32 = (*p32.s.list_count + 63u) / 64u, n64 = (*p64.s.list_count + 63u) / 64u;
     Counters cnt;
     const uint64_t t0 = p32.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t* lcol = nullptr;
+    if constexpr (LT) {
+        lcol = lds + sizeof(MemoLds<MODEL, G32>) / 4u + lane;
+        for (uint32_t e = 0; e < kLdsEntries; ++e) lcol[e * 8u * C_LANES] = kNoHistory;
+    }
     for (uint64_t grp = blockIdx.x; grp < n32 + n64; grp += gridDim.x) {
+        unsigned long long* q = p32.stats && grp < p32.stats_groups ? p32.stats + grp * 8u : nullptr;
         if (grp < n32) {
-            memo_group<MODEL, G32>(p32, grp * 64u, *reinterpret_cast<MemoLds<MODEL, G32>*>(lds), cnt, t0, lane);
-        } else if (wide) {
-            memo_group<MODEL, G64>(p64, (grp - n32) * 64u, *reinterpret_cast<MemoLds<MODEL, G64>*>(lds), cnt, t0,
-                                   lane);
+            auto& L = *reinterpret_cast<MemoLds<MODEL, G32>*>(lds);
+            if (q) memo_group<MODEL, G32, LT, true>(p32, grp * 64u, L, lcol, cnt, t0, lane, q);
+            else memo_group<MODEL, G32, LT, false>(p32, grp * 64u, L, lcol, cnt, t0, lane, q);
+        } else if (!LT && wide) {
+            auto& L = *reinterpret_cast<MemoLds<MODEL, G64>*>(lds);
+            if (q) memo_group<MODEL, G64, false, true>(p64, (grp - n32) * 64u, L, lcol, cnt, t0, lane, q);
+            else memo_group<MODEL, G64, false, false>(p64, (grp - n32) * 64u, L, lcol, cnt, t0, lane, q);
         } else {
             const uint64_t idx = (grp - n32) * 64u + lane;
             const bool in = idx < *p64.s.list_count;
@@ -274,16 +355,27 @@ __global__ __launch_bounds__(C_LANES, 3) void memo_search(MemoArgs p32, MemoArgs
     cnt.flush(p32.s.buckets, lane);
 }
 
-hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s) {
-    const bool bank = p32.s.model_id == QSMD_MODEL_BANK;
-    const size_t lds = wide ? (bank ? sizeof(MemoLds<QSMD_MODEL_BANK, G64>) : sizeof(MemoLds<QSMD_MODEL_TICKET, G64>))
-                            : (bank ? sizeof(MemoLds<QSMD_MODEL_BANK, G32>) : sizeof(MemoLds<QSMD_MODEL_TICKET, G32>));
-    if (bank)
-        hipLaunchKernelGGL((memo_search<QSMD_MODEL_BANK>), dim3(grid), dim3(C_LANES), lds, s, p32, p64, wide ? 1u : 0u);
-    else
-        hipLaunchKernelGGL((memo_search<QSMD_MODEL_TICKET>), dim3(grid), dim3(C_LANES), lds, s, p32, p64,
-                           wide ? 1u : 0u);
+template <uint32_t MODEL, bool LT>
+static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s) {
+    const size_t lds = LT ? sizeof(MemoLds<MODEL, G32>) + (size_t)kLdsEntries * 8u * C_LANES * 4u
+                          : (wide ? sizeof(MemoLds<MODEL, G64>) : sizeof(MemoLds<MODEL, G32>));
+    if constexpr (LT) {   // beyond the default 64 KB of dynamic LDS
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&memo_search<MODEL, true>),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (attr != hipSuccess) return attr;
+    }
+    hipLaunchKernelGGL((memo_search<MODEL, LT>), dim3(grid), dim3(C_LANES), lds, s, p32, p64, wide ? 1u : 0u);
     return hipGetLastError();
+}
+
+hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool lds_tables,
+                       hipStream_t s) {
+    const bool lt = lds_tables && !wide;
+    if (p32.s.model_id == QSMD_MODEL_BANK)
+        return lt ? launch_memo_t<QSMD_MODEL_BANK, true>(p32, p64, grid, wide, s)
+                  : launch_memo_t<QSMD_MODEL_BANK, false>(p32, p64, grid, wide, s);
+    return lt ? launch_memo_t<QSMD_MODEL_TICKET, true>(p32, p64, grid, wide, s)
+              : launch_memo_t<QSMD_MODEL_TICKET, false>(p32, p64, grid, wide, s);
 }
 
 }  // namespace qsmd

@@ -96,7 +96,7 @@ def test_random_any_shape(ctx, model):
 
 
 DEFAULTS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 1, "wave_budget": 16, "wave_max": 16384,
-            "split_budget": 1024, "memo_lane_entries": 256, "memo_grid": 4096, "split_xmemo": 1}
+            "split_budget": 1024, "memo_lane_entries": 256, "memo_grid": 4096, "split_xmemo": 1, "memo_lds": 1}
 
 
 @pytest.fixture
@@ -186,12 +186,13 @@ LANE_CASES = [("bank_4x16_bugs", 50000, 64, 0), ("bank_4x16_bugs", 20000, 8, 300
 
 @pytest.mark.parametrize("name,n,budget,max_nodes", LANE_CASES)
 @pytest.mark.parametrize("entries", [128, 2])
-def test_lane_mode(ctx, knobs, name, n, budget, max_nodes, entries):
-    """Lane mode of the heavy stage (exact-count state memo in a private HBM
-    table per lane): verdicts, node counts and witnesses must equal the
-    reference's.  2 entries: constant replacement; max_nodes: the budget
-    falls inside reused subtrees."""
-    knobs(heavy_mode=1, memo_lane_entries=entries, stage0_budget=budget, stage0w_budget=budget)
+@pytest.mark.parametrize("lds", [0, 2])
+def test_lane_mode(ctx, knobs, name, n, budget, max_nodes, entries, lds):
+    """Lane mode of the heavy stage (exact-count state memo in a private
+    table per lane, in HBM or, lds=2, in LDS): verdicts, node counts and
+    witnesses must equal the reference's.  2 entries: constant replacement;
+    max_nodes: the budget falls inside reused subtrees."""
+    knobs(heavy_mode=1, memo_lane_entries=entries, stage0_budget=budget, stage0w_budget=budget, memo_lds=lds)
     hdr, ev, _ = gen.generate_config(name, 5, n)
     _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
 

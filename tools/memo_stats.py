@@ -1,0 +1,86 @@
+"""Heavy-stage (lane mode) diagnostics on a generated configuration: per
+group of 64 histories, the wall time from its start to its staging and to its
+last history, the DFS iterations of its longest lane, memo hits and shader
+cycles per iteration (memo_stats_ptr; one diagnostic call after warm-up).
+
+    python tools/memo_stats.py bank_4x16 1000000 [param=value ...]
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "quickcheck-state-machine-distributed_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from qsmd import device, gen  # noqa: E402
+
+
+def main():
+    name, n = sys.argv[1], int(sys.argv[2])
+    ctx = device.Context(0)
+    for kv in sys.argv[3:]:
+        k, v = kv.split("=")
+        ctx.set_param(k, int(v))
+    dev = torch.device("cuda:0")
+    hdr, ev, _ = gen.generate_config(name, 0, n, threads=16)
+    mid = gen.CONFIGS[name]["model_id"]
+    d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
+    d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
+    d_st = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_nd = torch.empty(n, dtype=torch.int64, device=dev)
+    groups = (n + 63) // 64
+    stats = torch.zeros(groups * 8, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def call():
+        ctx.check_device(mid, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st.data_ptr(), d_nd.data_ptr(),
+                         stream=stream)
+
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    ctx.timing_reset()
+    ctx.set_param("memo_stats_groups", groups)
+    ctx.set_param("memo_stats_ptr", stats.data_ptr())
+    call()
+    torch.cuda.synchronize()
+    ctx.set_param("memo_stats_ptr", 0)
+    s0, dev_ms = ctx.timing_read()
+    q = stats.view(groups, 8).cpu().numpy().astype(np.int64)
+    q = q[q[:, 6] > 0]
+    if len(q) == 0:
+        print(json.dumps({"groups": 0}))
+        return
+    t0 = q[:, 0].min()
+    start = (q[:, 0] - t0) / 100.0          # s_memrealtime: 100 MHz -> us
+    staged = (q[:, 1] - q[:, 0]) / 100.0
+    span = (q[:, 2] - q[:, 0]) / 100.0
+    end = (q[:, 2] - t0) / 100.0
+    it = np.maximum(q[:, 3], 1)
+    cyc_per_it = q[:, 7] / it
+    worst = int(np.argmax(end))
+    out = {
+        "config": name, "histories": n, "groups": int(len(q)), "heavy_histories": int(q[:, 6].sum()),
+        "call_device_us": round(1e3 * float(dev_ms[-1]), 1), "stage0_us": round(1e3 * float(s0[-1]), 1),
+        "stage_span_us": round(float(end.max()), 1),
+        "group_start_us_max": round(float(start.max()), 1),
+        "staging_us_median": round(float(np.median(staged)), 2),
+        "group_span_us": {"median": round(float(np.median(span)), 1), "max": round(float(span.max()), 1)},
+        "max_iterations": {"median": int(np.median(q[:, 3])), "max": int(q[:, 3].max())},
+        "iterations_total": int(q[:, 4].sum()),
+        "memo_hits_total": int(q[:, 5].sum()),
+        "cycles_per_iteration": {"median": round(float(np.median(cyc_per_it)), 0),
+                                 "of_longest_group": round(float(cyc_per_it[worst]), 0)},
+        "longest_group": {"start_us": round(float(start[worst]), 1), "staging_us": round(float(staged[worst]), 2),
+                          "span_us": round(float(span[worst]), 1), "max_iterations": int(q[worst, 3]),
+                          "histories": int(q[worst, 6])},
+    }
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
