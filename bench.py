@@ -225,7 +225,7 @@ def reference_shaped(seconds):
 
 def extra_configs(dev, S, knobs):
     """Bounded runs of BASELINE configs 1, 3, 5 (same in-flight step as the
-    headline) and 4 (one adversarial 8 x 64 TicketDispenser history, memo
+    headline, the library's stage-0 budget) and 4 (one adversarial 8 x 64 TicketDispenser history, memo
     mode), each checked against the oracle on a sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_c
@@ -273,7 +273,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra BASELINE configs")
     ap.add_argument("--stage0-budget", type=int, default=None,
-                    help="stage-0 node budget (default 40 with calls in flight, the library's otherwise)")
+                    help="stage-0 node budget (default 26 with calls in flight, the library's otherwise)")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
                     help="qsmd_set_param on every context (tuning; repeatable)")
     ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")
@@ -343,7 +343,10 @@ def main():
     log(f"[rank {rank}] generated {n} histories ({'device' if args.device_gen else 'host'}) "
         f"in {time.perf_counter() - t:.2f}s")
 
-    budget0 = args.stage0_budget if args.stage0_budget is not None else (40 if S > 1 else -1)
+    # with calls in flight the heavy stage of one call overlaps the next call's
+    # stage 0, so a lower stage-0 budget pays: 26 measured best on config 2
+    # (6.14e9 vs 5.93e9 at 40 and 5.45e9 at 20; tools/gpu/ab_params.sh)
+    budget0 = args.stage0_budget if args.stage0_budget is not None else (26 if S > 1 else -1)
     knobs = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in args.param]
     # with calls in flight the heavy stage keeps its memo tables in HBM: the
     # LDS tables (the library's choice for a short heavy list, best for one

@@ -33,12 +33,15 @@ def main():
             k, v = kv.split("=")
             ctx.set_param(k, int(v))
         times = []
+        ctx.timing_reset()
         for _ in range(args.reps):
             t = time.perf_counter()
             st, nd, _, _ = ctx.check_arrays(1, h, e, flags=device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_MEMO)
             times.append(time.perf_counter() - t)
+        _, call_ms = ctx.timing_read()
         ctx.close()
         print(json.dumps({"case": case or "default", "bug": args.bug, "ms_median": round(1e3 * float(np.median(times[2:])), 3),
+                          "device_ms_median": round(float(np.median(call_ms[2:])), 3),
                           "verdict": int(st[0]), "oracle": int(st_o[0]), "explored": int(nd[0]),
                           "oracle_explored": int(nd_o[0])}), flush=True)
 
