@@ -198,15 +198,13 @@ struct StackN {
     }
     // push v (< 256) when c: one v_perm per word with a per-lane byte
     // selector (the shifted word when c, the word itself otherwise)
+    // (in place, top word first: no temporaries)
     __device__ __forceinline__ void push_if(bool c, uint32_t v) {
         const uint32_t keep = 0x07060504u;
         const uint32_t sel0 = c ? 0x06050400u : keep, sel = c ? 0x06050403u : keep;
-        uint32_t n[NW];
-        n[0] = __builtin_amdgcn_perm(w[0], v, sel0);
 #pragma unroll
-        for (int q = 1; q < NW; ++q) n[q] = __builtin_amdgcn_perm(w[q], w[q - 1], sel);
-#pragma unroll
-        for (int q = 0; q < NW; ++q) w[q] = n[q];
+        for (int q = NW - 1; q >= 1; --q) w[q] = __builtin_amdgcn_perm(w[q], w[q - 1], sel);
+        w[0] = __builtin_amdgcn_perm(w[0], v, sel0);
     }
 };
 

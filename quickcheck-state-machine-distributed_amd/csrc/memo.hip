@@ -359,9 +359,9 @@ template <uint32_t MODEL, bool LT>
 static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s) {
     const size_t lds = LT ? sizeof(MemoLds<MODEL, G32>) + (size_t)kLdsEntries * 8u * C_LANES * 4u
                           : (wide ? sizeof(MemoLds<MODEL, G64>) : sizeof(MemoLds<MODEL, G32>));
-    if constexpr (LT) {   // beyond the default 64 KB of dynamic LDS
-        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&memo_search<MODEL, true>),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if constexpr (LT) {   // beyond the default 64 KB of dynamic LDS (set on every launch: per device)
+        const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&memo_search<MODEL, true>),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (attr != hipSuccess) return attr;
     }
     hipLaunchKernelGGL((memo_search<MODEL, LT>), dim3(grid), dim3(C_LANES), lds, s, p32, p64, wide ? 1u : 0u);

@@ -1,13 +1,14 @@
 #!/bin/bash
-# A/B of bench.py parameter sets on one box, alternated (diagnostic):
-#   tools/gpu/ab_params.sh ROUNDS "TAG|ARGS" "TAG|ARGS" ...
+# A/B of bench.py settings on one box, alternated (diagnostic):
+#   tools/gpu/ab_params.sh ROUNDS "TAG|ENV|ARGS" ...
+# ENV: space-separated VAR=VALUE (e.g. QSMD_LIB_PATH=ablib/x.so), may be empty.
 # Each run: bench.py --no-cpu-baseline --no-extra ARGS; prints TAG value stage0/call means.
 R=$1; shift
 mkdir -p gpurun_out/abp
 for r in $(seq 1 "$R"); do
   for spec in "$@"; do
-    tag=${spec%%|*}; args=${spec#*|}
-    timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-extra $args > gpurun_out/abp/$tag.$r.json 2> gpurun_out/abp/$tag.$r.err
+    tag=${spec%%|*}; rest=${spec#*|}; envs=${rest%%|*}; args=${rest#*|}
+    env $envs timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-extra $args > gpurun_out/abp/$tag.$r.json 2> gpurun_out/abp/$tag.$r.err
     rc=$?
     if [ $rc -ne 0 ]; then echo "$tag rc=$rc"; exit $rc; fi
     python3 -c "import json,sys; d=json.load(open('gpurun_out/abp/$tag.$r.json')); print('$tag', '%.4g' % d['value'], '%.1f %.1f' % (1e3*d['device_ms']['stage0_mean'], 1e3*d['device_ms']['call_mean']))"
