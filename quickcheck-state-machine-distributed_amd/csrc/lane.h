@@ -317,89 +317,46 @@ __device__ __forceinline__ void stage_packed(const SearchArgs& a, uint32_t N0, u
 // only candidate of pid p is its first remaining invocation, and its
 // response is the next response of p, so the pair is static).  The pair
 // index is OR-ed into the invocation word (r field).
-//
-// Two passes over the column, 8 events at a time with the event index
-// wave-uniform (the wavefront's longest history bounds the loop; no indexed
-// registers, no per-event branches, no LDS atomics):
-//   1. the masks: RESP, the pid bit slices, the marker events;
-//   2. per event, its pid's events (bit-slice compare) give the next and the
-//      previous event of the same pid: an invocation's r is the next one
-//      (a response in a paired history); the history is paired iff no
-//      event's next event has its own kind and no response is its pid's
-//      first event.
-// Words beyond n_ev (stale) are masked out by ALL and written back unchanged.
 template <class G = G32>
 __device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane, uint32_t n_ev, uint32_t n_pid,
                                             StagedT<typename G::M>& s) {
     using M = typename G::M;
-    constexpr uint32_t U = 8;
-    // the longest history of the lanes that call (a ballot max: the callers
-    // may be a subset of the wavefront)
-    const uint32_t n_cl = min(n_ev, (uint32_t)G::EV);
-    uint32_t n_max = 0;
-#pragma unroll
-    for (int b = 6; b >= 0; --b) {
-        const uint32_t t = n_max | (1u << b);
-        n_max = __ballot(n_cl >= t) ? t : n_max;
-    }
-    const M ALL = mask_below(n_ev, (M)0);
-    M RESP = 0, P0 = 0, P1 = 0, P2 = 0, BAD = 0, WIDE = 0;
+    uint32_t open = 0u, ps_lo = 0u, ps_hi = 0u, unpaired = 0u, bad = 0u, wide = 0u;
 #pragma unroll 1
-    for (uint32_t c0 = 0; c0 < n_max; c0 += U) {
-        uint32_t W[U];
+    for (uint32_t c0 = 0; c0 < (uint32_t)G::EV; c0 += 32u) {
+    if (c0 >= n_ev) break;
+    uint32_t W[32];                  // the chunk's words first (the pair ORs below go to earlier words)
 #pragma unroll
-        for (uint32_t k = 0; k < U; ++k) W[k] = s_ev[c0 + k][lane];
+    for (uint32_t k = 0; k < 32u; ++k) W[k] = s_ev[c0 + k][lane];
 #pragma unroll
-        for (uint32_t k = 0; k < U; ++k) {
-            const uint32_t e = c0 + k, w = W[k];
-            RESP |= (M)((w >> 3) & 1u) << e;
-            P0 |= (M)(w & 1u) << e;
-            P1 |= (M)((w >> 1) & 1u) << e;
-            P2 |= (M)((w >> 2) & 1u) << e;
-            const uint32_t mk = w & 0x78u;
-            BAD |= (M)(mk == MARK_BAD ? 1u : 0u) << e;
-            WIDE |= (M)(mk == MARK_WIDE ? 1u : 0u) << e;
-        }
+    for (uint32_t k = 0; k < 32u; ++k) {
+        const uint32_t e = c0 + k;
+        if (e >= n_ev) break;
+        const uint32_t w = W[k];
+        const M bit = (M)1 << e;
+        const uint32_t p = w & 7u, resp = (w >> 3) & 1u, mk = w & 0x78u;
+        bad |= ((mk == MARK_BAD) | (p >= n_pid)) ? 1u : 0u;
+        wide |= mk == MARK_WIDE ? 1u : 0u;
+        s.RESP |= resp ? bit : (M)0;
+        s.INV |= resp ? (M)0 : bit;
+        s.P0 |= (w & 1u) ? bit : (M)0;
+        s.P1 |= (w & 2u) ? bit : (M)0;
+        s.P2 |= (w & 4u) ? bit : (M)0;
+        // pairing: ps = event index of the open invocation per pid (8 bits each)
+        const uint32_t ob = (open >> p) & 1u, sh = (p & 3u) * 8u;
+        const bool hi = p >= 4u;
+        const uint32_t j = ((hi ? ps_hi : ps_lo) >> sh) & (uint32_t)(G::EV - 1);
+        unpaired |= resp ? (ob ^ 1u) : ob;
+        open ^= (resp ? ob : (ob ^ 1u)) << p;                 // inv opens, its resp closes
+        const uint32_t ins = (ps_lo & ~(0xFFu << sh)) | (e << sh), insh = (ps_hi & ~(0xFFu << sh)) | (e << sh);
+        ps_lo = (!resp && !hi) ? ins : ps_lo;
+        ps_hi = (!resp && hi) ? insh : ps_hi;
+        if (resp & ob) atomicOr(&s_ev[j][lane], e << 13);
     }
-    RESP &= ALL;
-    P0 &= ALL;
-    P1 &= ALL;
-    P2 &= ALL;
-    const M INV = ALL & ~RESP;
-    // events whose pid is >= n_pid (pid q's events from the bit slices)
-    M GEP = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < 8u; ++q) {
-        const M pq = ((q & 1u) ? P0 : ~P0) & ((q & 2u) ? P1 : ~P1) & ((q & 4u) ? P2 : ~P2) & ALL;
-        GEP |= q >= n_pid ? pq : (M)0;
     }
-    M UNP = 0;
-#pragma unroll 1
-    for (uint32_t c0 = 0; c0 < n_max; c0 += U) {
-        uint32_t W[U];
-#pragma unroll
-        for (uint32_t k = 0; k < U; ++k) W[k] = s_ev[c0 + k][lane];
-#pragma unroll
-        for (uint32_t k = 0; k < U; ++k) {
-            const uint32_t e = c0 + k;
-            const M m0 = (M)0 - ((P0 >> e) & (M)1), m1 = (M)0 - ((P1 >> e) & (M)1), m2 = (M)0 - ((P2 >> e) & (M)1);
-            const M sp = ~((P0 ^ m0) | (P1 ^ m1) | (P2 ^ m2)) & ALL;   // the events of e's pid
-            const M nxt = sp & mask_above(e, (M)0), lb = nxt & ((M)0 - nxt);
-            const bool isr = ((RESP >> e) & (M)1) != (M)0;
-            const bool first = (sp & mask_below(e, (M)0)) == (M)0;
-            UNP |= isr ? ((lb & RESP) | (M)(first ? 1u : 0u)) : (lb & INV);
-            const uint32_t r = (!isr && nxt != (M)0) ? m_ctz(nxt) : 0u;
-            s_ev[e][lane] = W[k] | (r << 13);
-        }
-    }
-    s.INV = INV;
-    s.RESP = RESP;
-    s.P0 = P0;
-    s.P1 = P1;
-    s.P2 = P2;
-    s.ok = ((BAD & ALL) | GEP) == (M)0;
-    s.fits = (WIDE & ALL) == (M)0;
-    s.paired = UNP == (M)0;
+    s.ok = bad == 0u;
+    s.fits = wide == 0u;
+    s.paired = unpaired == 0u;
 }
 
 // finish_lane for a history shared by the wavefront (csrc/wave.hip): every
