@@ -22,7 +22,7 @@
 // 64 histories per wavefront, staged together (coalesced 16-B loads for
 // packed batches), each searched with a node budget: a wavefront runs as
 // long as its slowest lane, so a history that exceeds the budget is appended
-// to the heavy list (csrc/wave.hip searches it with a whole wavefront).
+// to the heavy list (csrc/memo.hip searches it with the exact-count memo).
 // Histories outside the stage's bounds go to the next stage through a
 // wave-aggregated append to the defer list.
 #include <hip/hip_runtime.h>
@@ -147,13 +147,8 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
 #endif
         const bool search = status == -1;
         const uint32_t n_ev = H.n_ev;
-        // one specialised loop per wavefront: paired when every searched
-        // history of the wavefront is paired
-        if (__ballot(search && !dfs.paired) == 0ull) {
-            if (search) status = run_search<M_PAIRED>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
-        } else {
-            if (search) status = run_search<M_GENERAL>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
-        }
+        // the general path (pid masks): finish_lane does not pair (lane.h)
+        if (search) status = run_search<M_GENERAL>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
         note_failure(a, h, status);
         // over the stage budget (not the caller's): searched again by the heavy stage
         const bool heavy = tiered && status == QSMD_STATUS_BUDGET && dfs.nodes >= limit;

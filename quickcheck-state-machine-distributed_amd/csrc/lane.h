@@ -26,7 +26,9 @@ constexpr int32_t V19_MIN = -(1 << 18), V19_MAX = (1 << 18) - 1;   // model0 val
 //   invocation  pid 3 | 0 | code 3 | a 3 | b 3 | r 5 | val 14 (signed)
 //   response    pid 3 | 1 | code 3 | val 25 (signed)
 // r: in a paired history (every pid alternates invocation / response), the
-// index of the response paired with the invocation (0 = none: pending).
+// index of the response paired with the invocation (0 = none: pending);
+// filled only by wave mode's finish_shared (finish_lane leaves it 0: the
+// compact stages run the general path).
 // Staging writes a marker instead of an event it cannot hold: an invocation
 // with code 7 (not an encodable event: ENCODE_ERROR) or code 6 (a value
 // outside the ranges above: the history goes to the next stage).
@@ -311,52 +313,64 @@ __device__ __forceinline__ void stage_packed(const SearchArgs& a, uint32_t N0, u
 }
 
 // Per lane, over its own column: the encoding checks (markers, pid <
-// n_pid), the register masks, and the pairing of every invocation with the
-// response of the same pid that follows it when every pid alternates
-// invocation / response (SURVEY.md §8a Lemma L1.4: in such a history the
-// only candidate of pid p is its first remaining invocation, and its
-// response is the next response of p, so the pair is static).  The pair
-// index is OR-ed into the invocation word (r field).
+// n_pid) and the register masks (RESP / INV, the pid bit slices), 8 events
+// at a time with the event index wave-uniform (the calling lanes' longest
+// history bounds the loop: no indexed registers, no per-event branches).
+// No pairing: the compact stages search every history on the general path
+// (pid masks), which costs less per DFS step than pairing the invocations
+// at staging costs per event (A/B in flight, config 2: 6.44e9 vs 6.10e9
+// histories/s).  Words beyond n_ev (stale) are masked out by ALL.
 template <class G = G32>
 __device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane, uint32_t n_ev, uint32_t n_pid,
                                             StagedT<typename G::M>& s) {
     using M = typename G::M;
-    uint32_t open = 0u, ps_lo = 0u, ps_hi = 0u, unpaired = 0u, bad = 0u, wide = 0u;
+    constexpr uint32_t U = 8;
+    // a ballot max: the callers may be a subset of the wavefront
+    const uint32_t n_cl = min(n_ev, (uint32_t)G::EV);
+    uint32_t n_max = 0;
+#pragma unroll
+    for (int b = 6; b >= 0; --b) {
+        const uint32_t t = n_max | (1u << b);
+        n_max = __ballot(n_cl >= t) ? t : n_max;
+    }
+    const M ALL = mask_below(n_ev, (M)0);
+    M RESP = 0, P0 = 0, P1 = 0, P2 = 0, BAD = 0, WIDE = 0;
 #pragma unroll 1
-    for (uint32_t c0 = 0; c0 < (uint32_t)G::EV; c0 += 32u) {
-    if (c0 >= n_ev) break;
-    uint32_t W[32];                  // the chunk's words first (the pair ORs below go to earlier words)
+    for (uint32_t c0 = 0; c0 < n_max; c0 += U) {
+        uint32_t W[U];
 #pragma unroll
-    for (uint32_t k = 0; k < 32u; ++k) W[k] = s_ev[c0 + k][lane];
+        for (uint32_t k = 0; k < U; ++k) W[k] = s_ev[c0 + k][lane];
 #pragma unroll
-    for (uint32_t k = 0; k < 32u; ++k) {
-        const uint32_t e = c0 + k;
-        if (e >= n_ev) break;
-        const uint32_t w = W[k];
-        const M bit = (M)1 << e;
-        const uint32_t p = w & 7u, resp = (w >> 3) & 1u, mk = w & 0x78u;
-        bad |= ((mk == MARK_BAD) | (p >= n_pid)) ? 1u : 0u;
-        wide |= mk == MARK_WIDE ? 1u : 0u;
-        s.RESP |= resp ? bit : (M)0;
-        s.INV |= resp ? (M)0 : bit;
-        s.P0 |= (w & 1u) ? bit : (M)0;
-        s.P1 |= (w & 2u) ? bit : (M)0;
-        s.P2 |= (w & 4u) ? bit : (M)0;
-        // pairing: ps = event index of the open invocation per pid (8 bits each)
-        const uint32_t ob = (open >> p) & 1u, sh = (p & 3u) * 8u;
-        const bool hi = p >= 4u;
-        const uint32_t j = ((hi ? ps_hi : ps_lo) >> sh) & (uint32_t)(G::EV - 1);
-        unpaired |= resp ? (ob ^ 1u) : ob;
-        open ^= (resp ? ob : (ob ^ 1u)) << p;                 // inv opens, its resp closes
-        const uint32_t ins = (ps_lo & ~(0xFFu << sh)) | (e << sh), insh = (ps_hi & ~(0xFFu << sh)) | (e << sh);
-        ps_lo = (!resp && !hi) ? ins : ps_lo;
-        ps_hi = (!resp && hi) ? insh : ps_hi;
-        if (resp & ob) atomicOr(&s_ev[j][lane], e << 13);
+        for (uint32_t k = 0; k < U; ++k) {
+            const uint32_t e = c0 + k, w = W[k];
+            RESP |= (M)((w >> 3) & 1u) << e;
+            P0 |= (M)(w & 1u) << e;
+            P1 |= (M)((w >> 1) & 1u) << e;
+            P2 |= (M)((w >> 2) & 1u) << e;
+            const uint32_t mk = w & 0x78u;
+            BAD |= (M)(mk == MARK_BAD ? 1u : 0u) << e;
+            WIDE |= (M)(mk == MARK_WIDE ? 1u : 0u) << e;
+        }
     }
+    RESP &= ALL;
+    P0 &= ALL;
+    P1 &= ALL;
+    P2 &= ALL;
+    // events whose pid is >= n_pid (pid q's events from the bit slices)
+    M GEP = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 8u; ++q) {
+        const M pq = ((q & 1u) ? P0 : ~P0) & ((q & 2u) ? P1 : ~P1) & ((q & 4u) ? P2 : ~P2) & ALL;
+        GEP |= q >= n_pid ? pq : (M)0;
     }
-    s.ok = bad == 0u;
-    s.fits = wide == 0u;
-    s.paired = unpaired == 0u;
+    s.INV = ALL & ~RESP;
+    s.RESP = RESP;
+    s.P0 = P0;
+    s.P1 = P1;
+    s.P2 = P2;
+    s.ok = ((BAD & ALL) | GEP) == (M)0;
+    s.fits = (WIDE & ALL) == (M)0;
+    s.paired = false;
 }
 
 // finish_lane for a history shared by the wavefront (csrc/wave.hip): every

@@ -276,7 +276,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
         uint32_t iter = 0;
         do {
             const bool was = skip;
-            status = memo_step<MODEL, G, M_LANE, LT>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch, mask,
+            status = memo_step<MODEL, G, M_GENERAL, LT>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch, mask,
                                                  &L.entry[0][lane], skip);
             if constexpr (ST) hits += (!was && skip) ? 1u : 0u;
             ++iter;
