@@ -373,6 +373,11 @@ int qsmd_timing_read(qsmd_ctx* ctx, float* stage0_ms, float* call_ms, uint64_t m
  * call (waits for it). */
 int qsmd_probe_read(qsmd_ctx* ctx, uint32_t* out4);
 
+/* Whether the time limit (qsmd_set_time_limit_ms) fired in the most recent
+ * check call (waits for it): *out = 1 when some of its QSMD_STATUS_BUDGET
+ * results come from the time limit rather than max_nodes, else 0. */
+int qsmd_timed_out(qsmd_ctx* ctx, int* out);
+
 #ifdef __cplusplus
 }
 #endif

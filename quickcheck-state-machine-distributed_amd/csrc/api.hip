@@ -70,7 +70,7 @@ struct qsmd_ctx {
     uint64_t heavy_mode = 1;
     uint64_t wave_max = 16384;
     bool lane_mode = false;
-    uint32_t* probe_host = nullptr;    // pinned: [defer, heavy32, heavy64, giant] of the last finished call
+    uint32_t* probe_host = nullptr;    // pinned: [defer, heavy32, heavy64, giant, timed] of the last finished call
     uint32_t* debug_host = nullptr;    // QSMD_SYNC_STAGES: giant-stage heartbeat (pinned)
     // lane mode's tables: one per lane slot of the memo grid
     uint64_t memo_grid = 4096;         // heavy stage (lane mode): workgroups at most; one private table each
@@ -821,6 +821,14 @@ int qsmd_probe_read(qsmd_ctx* c, uint32_t* out4) {
     std::lock_guard<std::mutex> g(c->mu);
     quiesce(c);
     for (int i = 0; i < 4; ++i) out4[i] = c->probe_host[i];
+    return QSMD_OK;
+}
+
+int qsmd_timed_out(qsmd_ctx* c, int* out) {
+    if (!c || !out) return QSMD_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    quiesce(c);
+    *out = c->probe_host[C_TIMED] != 0u ? 1 : 0;
     return QSMD_OK;
 }
 

@@ -63,6 +63,7 @@ EXPORTS = {
     "qsmd_set_stage0_grid": (_I, [_P, _U64]),
     "qsmd_set_stage0_budget": (_I, [_P, _U64]),
     "qsmd_probe_read": (_I, [_P, _P]),
+    "qsmd_timed_out": (_I, [_P, _P]),
     "qsmd_wellformed_batch": (_I, [_P, _P, _U64, _P, _U64, _P, _U32, _P]),
     "qsmd_wellformed_batch_device": (_I, [_P, _P, _U64, _P, _U64, _P, _U32, _P, _P]),
     "qsmd_gen_batch_device": (_I, [_P, _P, _U64, _U64, _U32, _P, _P, _P, _P]),   # include/qsmd_gen.h
@@ -201,6 +202,11 @@ class Context:
         self._check(self._lib.qsmd_last_kernel_ms(self._h, ctypes.byref(ms)), "qsmd_last_kernel_ms")
         return float(ms.value)
 
+    def set_time_limit_ms(self, ms):
+        """qsmd_set_time_limit_ms: the safety net's wall time per search launch
+        (0 disables)."""
+        self._check(self._lib.qsmd_set_time_limit_ms(self._h, int(ms)), "qsmd_set_time_limit_ms")
+
     def set_stage0_grid(self, max_blocks):
         self._check(self._lib.qsmd_set_stage0_grid(self._h, int(max_blocks)), "qsmd_set_stage0_grid")
 
@@ -299,6 +305,14 @@ class Context:
         out = (ctypes.c_uint32 * 4)()
         self._check(self._lib.qsmd_probe_read(self._h, out), "qsmd_probe_read")
         return dict(zip(("deferred", "heavy32", "heavy64", "giants"), (int(x) for x in out)))
+
+    def timed_out(self):
+        """True when the time limit fired in the most recent check call (its
+        QSMD_STATUS_BUDGET results then include unfinished searches, not only
+        max_nodes ones)."""
+        out = ctypes.c_int(0)
+        self._check(self._lib.qsmd_timed_out(self._h, ctypes.byref(out)), "qsmd_timed_out")
+        return bool(out.value)
 
     def timing_reset(self):
         self._check(self._lib.qsmd_timing_reset(self._h), "qsmd_timing_reset")

@@ -248,3 +248,25 @@ def test_ticket_8x64_batch(ctx, xmemo, split):
             _compare(ctx, models.MODEL_TICKET, hdr, ev, max_nodes=10**7)
     finally:
         ctx.set_param("split_xmemo", 1)
+
+
+def test_time_limit_is_reported(ctx):
+    """The safety net (qsmd_set_time_limit_ms) is told apart from max_nodes:
+    an adversarial 6 x 30 history without the exact memo (8.8e13 reference
+    nodes) cannot finish in 20 ms, so the call reports BUDGET and
+    qsmd_timed_out says the time limit fired; the next call, under the
+    default limit, finishes and says it did not."""
+    h, e, _ = gen.adversarial_ticket(6, 30, bug=True)
+    ctx.set_param("split_xmemo", 0)
+    ctx.set_time_limit_ms(20)
+    try:
+        st, _, _, _ = ctx.check_arrays(models.MODEL_TICKET, h, e)
+        assert int(st[0]) == codec.STATUS_BUDGET
+        assert ctx.timed_out()
+    finally:
+        ctx.set_time_limit_ms(60000)
+        ctx.set_param("split_xmemo", 1)
+    h2, e2, _ = gen.adversarial_ticket(4, 17, bug=True)
+    st, nd, _, _ = ctx.check_arrays(models.MODEL_TICKET, h2, e2)
+    assert (int(st[0]), int(nd[0])) == (codec.STATUS_NONLIN, 923201)
+    assert not ctx.timed_out()
