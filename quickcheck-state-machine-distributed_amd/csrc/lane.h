@@ -486,7 +486,11 @@ struct LaneDFS {
             const int32_t m = c_ival<G>(cj);
             const uint32_t pa = (st >> JB) & 1u, pb = (st >> (JB + 1u)) & 1u;
             const uint32_t tr = code == QSMD_BANK_TRANSFER ? 1u : 0u;
-            const int32_t ba = s_bal[ia][lane], bb = s_bal[ib][lane];
+            int32_t ba = s_bal[ia][lane], bb = s_bal[ib][lane];
+            // both reads in flight together: without this the compiler sinks
+            // ba's read into a branch on the pre-op `exists a` bit, a second
+            // serial LDS round trip per backtrack
+            asm volatile("" : "+v"(ba), "+v"(bb));
             // undo Transfer's deposit on b, then the step on a
             const int32_t rb = (pb | (ia == ib)) ? bb - m : 0;
             const int32_t cur_a = (tr & (ia == ib)) ? rb : ba;
