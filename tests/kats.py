@@ -31,6 +31,41 @@ KATS = {
     # the same request answered by a non-Balance constructor does not force Map.!
     "KAT9_bank_no_error": ("bank", [
         ("a", L(("CheckBalance", "a"))), ("a", R("AccountDoesntExist"))], "nonlin", 1),
+    # Bank KATs 10-16, hand-derived from test/Bank.hs:92-131 (next', invariant,
+    # post) and src/Linearisability.hs:52-69; each pins one clause:
+    # Withdraw on an absent account inserts +m (insertWith keeps the new value)
+    "KAT10_bank_withdraw_creates": ("bank", [
+        ("a", L(("Withdraw", "a", 5))), ("a", R("InsufficientFunds")),
+        ("a", L(("CheckBalance", "a"))), ("a", R(("Balance", 5)))], "lin", 2),
+    # next' ignores the response (the refused Withdraw still subtracts), and
+    # the invariant is checked on the pre-state of the next step
+    "KAT11_bank_invariant_prestate": ("bank", [
+        ("a", L(("OpenAccount", "a"))), ("a", R("AccountCreated")),
+        ("a", L(("Withdraw", "a", 5))), ("a", R("InsufficientFunds")),
+        ("a", L(("Deposit", "a", 1))), ("a", R("DepositMade"))], "nonlin", 3),
+    # Transfer = Withdraw then Deposit, on one account: absent -> +7 -> 14
+    "KAT12_bank_self_transfer": ("bank", [
+        ("a", L(("Transfer", "a", 7, "a"))), ("a", R("InsufficientFunds")),
+        ("a", L(("CheckBalance", "a"))), ("a", R(("Balance", 14)))], "lin", 2),
+    # OpenAccount on an existing account: AlreadyExists, balance kept
+    "KAT13_bank_open_existing": ("bank", [
+        ("a", L(("Deposit", "a", 3))), ("a", R("DepositMade")),
+        ("a", L(("OpenAccount", "a"))), ("a", R("AccountAlreadyExists")),
+        ("a", L(("CheckBalance", "a"))), ("a", R(("Balance", 3)))], "lin", 3),
+    # two concurrent operations, both orders tried and both fail: Deposit
+    # first expects WithdrawalMade; Withdraw first is refused, leaves -4, and
+    # the Deposit after it meets the broken invariant
+    "KAT14_bank_both_orders_fail": ("bank", [
+        ("a", L(("OpenAccount", "a"))), ("a", R("AccountCreated")),
+        ("a", L(("Deposit", "a", 10))), ("b", L(("Withdraw", "a", 4))),
+        ("a", R("DepositMade")), ("b", R("InsufficientFunds"))], "nonlin", 5),
+    # Map.! after a successful prefix: the error ends the search at node 2
+    "KAT15_bank_error_after_prefix": ("bank", [
+        ("a", L(("OpenAccount", "a"))), ("a", R("AccountCreated")),
+        ("b", L(("CheckBalance", "b"))), ("b", R(("Balance", 0)))], "error", 2),
+    # Nothing < Just m: a Transfer from an absent account must be refused
+    "KAT16_bank_nothing_below_just": ("bank", [
+        ("a", L(("Transfer", "a", 5, "b"))), ("a", R("TransferMade"))], "nonlin", 1),
 }
 
 # The trace text of the reference's example (test/TicketDispenser.hs:329-344),
