@@ -344,8 +344,8 @@ def main():
         f"in {time.perf_counter() - t:.2f}s")
 
     # with calls in flight the heavy stage of one call overlaps the next call's
-    # stage 0, so a lower stage-0 budget pays: 26 measured best on config 2
-    # (6.14e9 vs 5.93e9 at 40 and 5.45e9 at 20; tools/gpu/ab_params.sh)
+    # stage 0, so a lower stage-0 budget pays: 23-29 measured best on config 2
+    # (6.46-6.54e9 vs 6.28e9 at 40 and 5.81e9 at 20; tools/gpu/ab_params.sh)
     budget0 = args.stage0_budget if args.stage0_budget is not None else (26 if S > 1 else -1)
     knobs = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in args.param]
     # with calls in flight the heavy stage keeps its memo tables in HBM: the
