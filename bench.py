@@ -82,7 +82,8 @@ class InFlight:
     the previous call's tail leaves idle).  With RCCL the counters of R rounds
     of steps are all-reduced together, overlapping the next block."""
 
-    def __init__(self, dev, model_id, d_hdr, n, d_ev, n_ev, S, R, flags, use_dist, knobs, budget0, streams=None):
+    def __init__(self, dev, model_id, d_hdr, n, d_ev, n_ev, S, R, flags, use_dist, knobs, budget0, streams=None,
+                 host_group=None):
         self.dev, self.model_id, self.d_hdr, self.n, self.d_ev, self.n_ev = dev, model_id, d_hdr, n, d_ev, n_ev
         self.S, self.B, self.flags = S, R * S, flags
         self.ctxs = [device.Context(dev.index) for _ in range(S)]
@@ -97,6 +98,7 @@ class InFlight:
         # counters: [block parity][step of the block][8]; a row is reused two blocks later
         self.tot = torch.zeros(2, self.B, 8, dtype=torch.int64, device=dev)
         self.use_dist = use_dist
+        self.host_group = host_group
         self.comm = self.streams[S - 1] if use_dist else None   # RCCL adds its own stream: reuse a slot's
         self.do_ar = use_dist and os.environ.get("QSMD_BENCH_NOAR") != "1"
         self.done = [None, None]
@@ -138,7 +140,7 @@ class InFlight:
         self.drain()
         torch.cuda.synchronize(self.dev)
         if self.use_dist:
-            dist.barrier()
+            dist.barrier(group=self.host_group)
         torch.cuda.synchronize(self.dev)
         self.ctxs[0].timing_reset()
         t0 = time.perf_counter()
@@ -147,12 +149,12 @@ class InFlight:
         self.drain()
         torch.cuda.synchronize(self.dev)
         if self.use_dist:
-            dist.barrier()
+            dist.barrier(group=self.host_group)
         torch.cuda.synchronize(self.dev)
         elapsed = time.perf_counter() - t0
         if self.use_dist:
-            e = torch.tensor([elapsed], dtype=torch.float64, device=self.dev)
-            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            e = torch.tensor([elapsed], dtype=torch.float64)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.host_group)
             elapsed = float(e.item())
         return elapsed
 
@@ -290,6 +292,14 @@ def main():
                     help="PMC summary of the stage-0 kernel (profiles/summarize_pmc.py) for the roofline fields")
     args = ap.parse_args()
 
+    # stdout carries exactly one JSON line (rank 0): RCCL prints a version
+    # banner to file descriptor 1 when it creates its communicator, so fd 1
+    # goes to stderr for the whole run and the JSON line is written to a
+    # duplicate of the original stdout
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -316,12 +326,24 @@ def main():
         # after the slot streams and contexts exist: created eagerly at init
         # (device_id=dev, QSMD_BENCH_EAGER=1) it cost 38 % of one rank's
         # throughput with no collective issued (profiles/r02/rccl_sweep.txt).
+        # PyTorch's NCCL process group runs a watchdog and a heartbeat monitor
+        # thread; with them one rank on the RCCL path lost 5-7 % of its
+        # throughput even with no collective issued (5.09-5.40 vs 5.62-5.80e9,
+        # 20 steps); without them it is within the run-to-run spread.  The
+        # bench's collectives are bounded by gpurun / the driver's time limits.
+        os.environ.setdefault("TORCH_NCCL_ENABLE_MONITORING", "0")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
         if os.environ.get("QSMD_BENCH_BACKEND") == "gloo":
             dist.init_process_group("gloo")
         elif os.environ.get("QSMD_BENCH_EAGER") == "1":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("nccl")
+    # the bracketing barriers and the MAX over ranks of the timed region go
+    # over a host (gloo) group: after torch.cuda.synchronize() every rank's
+    # GPU work is done, and a host barrier costs no RCCL launch inside the
+    # window (the counters' all-reduce stays on RCCL)
+    host_group = dist.new_group(backend="gloo") if use_dist else None
 
     cfg = dict(gen.CONFIGS[args.config])
     model_id = cfg["model_id"]
@@ -356,7 +378,7 @@ def main():
         knobs.append(("memo_lds", 0))
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
     run = InFlight(dev, model_id, d_hdr, n, d_ev, len(ev), S, max(1, args.ar_rounds), flags, use_dist, knobs,
-                   budget0, streams)
+                   budget0, streams, host_group)
     elapsed = run.timed(args.steps, args.warmup)
     s0_ms, call_ms = run.ctxs[0].timing_read()
     st, nd, tot = run.results()
@@ -425,7 +447,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_extra:
         out["extra"] = {"configs": extra_configs(dev, S, knobs)}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if use_dist:
         dist.destroy_process_group()
 
