@@ -30,9 +30,8 @@
 #include "internal.h"
 #include "lane.h"
 
-// Diagnostic builds only (tools/build_variant.sh): 1 = stage 0 without the
-// search, 2 = also without finish_lane, 3 = also without the event loads,
-// 4 = no search and no finish_lane, the staged column folded (kept alive).
+// Diagnostic build only (tools/build_variant.sh): QSMD_DIAG_STAGE0=1 runs
+// stage 0 without the search (staging, masks and I/O alone).
 #ifndef QSMD_DIAG_STAGE0
 #define QSMD_DIAG_STAGE0 0
 #endif
@@ -89,19 +88,9 @@ __device__ __forceinline__ int stage_fresh(const SearchArgs& a, bool fresh, uint
     const uint32_t off0 = __builtin_amdgcn_readfirstlane(H.ev_off);
     const bool lane_uni = small && n_ev == N0 && H.ev_off == off0 + (uint32_t)lane * N0;
     const bool packed = F != 0ull && __ballot(fresh && !lane_uni) == 0ull && N0 > 0u;
-#if QSMD_DIAG_STAGE0 < 3
     if (packed) stage_packed<MODEL, G>(a, N0, off0, (uint32_t)__builtin_popcountll(F), s_ev, lane);
     else if (small) stage_lane<MODEL, G>(a, H, s_ev, lane);
-#endif
-#if QSMD_DIAG_STAGE0 < 2
     if (small) finish_lane<G>(s_ev, lane, n_ev, n_pid, s);
-#elif QSMD_DIAG_STAGE0 == 4
-    if (small) {   // keep the staged words alive: fold the lane's column
-        uint32_t x = 0;
-        for (uint32_t e = 0; e < n_ev; ++e) x ^= s_ev[e][lane];
-        s.ok = x != 0x12345u;
-    }
-#endif
     s.ok = s.ok && enc_ok;
 
     const bool defer = enc_ok && (!small || (s.ok && !s.fits));
