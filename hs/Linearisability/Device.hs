@@ -84,6 +84,8 @@ foreign import ccall safe "qsmd_open"
   c_open :: Ptr (Ptr QsmdCtx) -> CInt -> IO CInt
 foreign import ccall safe "qsmd_last_error"
   c_last_error :: Ptr QsmdCtx -> IO CString
+foreign import ccall safe "qsmd_timed_out"
+  c_timed_out :: Ptr QsmdCtx -> Ptr CInt -> IO CInt
 -- `safe`: a call can run for a long time and must not block the other
 -- capabilities of the -threaded RTS (package.yaml:48-51).
 foreign import ccall safe "qsmd_check_batch"
@@ -255,6 +257,14 @@ linearisableBatch m hists =
             throwIO (DeviceError ("qsmd_check_batch failed (" ++ show rc ++ "): " ++ msg))
           status <- peekArray nHist st
           ws     <- peekArray nEv wit
+          -- max_nodes is 0 here: a BUDGET status can only come from the
+          -- safety net (qsmd_set_time_limit_ms); say so rather than guess
+          when (4 `elem` status) $ alloca $ \tp -> do
+            _ <- c_timed_out ctx tp
+            timed <- peek tp
+            throwIO (DeviceError (if timed /= 0
+                                    then "the device time limit fired before every verdict was decided"
+                                    else "unexpected BUDGET status without a node limit"))
           return (zipWith3 (verdict ws) enc offs status)
   where
     enc   = map (encodeHistory m) hists
