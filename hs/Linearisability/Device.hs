@@ -366,26 +366,44 @@ linearisableDevice
 linearisableDevice transition postcondition model0 hist =
   unsafePerformIO (linearisableDeviceIO transition postcondition model0 hist)
 
--- | Replay a witness (SURVEY.md §8a Lemma L1): at each step the operation is
--- (pid p of the chosen invocation, its inv, the first remaining response of
--- p); the first remaining invocation and response of p are removed
--- (filter1 / findResponse, src/Linearisability.hs:30-50).
+-- | Replay a witness (SURVEY.md §8a Lemma L1) as a path of the reference's
+-- tree: each chosen invocation j must be a root of
+-- @interleavings rest@ -- a remaining invocation inside the
+-- 'takeInvocations' prefix (before the first remaining response,
+-- src/Linearisability.hs:25-28) whose pid has a remaining response
+-- (findResponse, :30-34); the operation is (its pid p, its inv, the first
+-- remaining response of p); the first remaining invocation and response of p
+-- are removed (filter1, :41,:47-50).  The path must end at a leaf (no root
+-- left: @any' [] = True@, :67), and the empty witness stands only for the
+-- empty history (@linearisable _ _ _ [] = True@, :59; a non-empty history
+-- with no root is False, :60).  A truncated witness, or one that starts an
+-- operation after a pending response, is rejected.
 replay
   :: Eq pid
   => (model -> Either inv resp -> model)
   -> (model -> inv -> resp -> Bool)
   -> model -> History pid inv resp -> [Int] -> Bool
-replay transition postcondition model0 hist = go model0 (zip [0 ..] hist)
+replay _ _ _ hist [] = null hist
+replay transition postcondition model0 hist ws0 = go model0 (zip [0 ..] hist) ws0
   where
-    go _ _ [] = True
-    go m rest (j : js) = case lookup j rest of
-      Just (pid, Left inv) -> case [ (k, r) | (k, (q, Right r)) <- rest, q == pid ] of
-        (k, resp) : _ ->
+    go _ rest [] = null (roots rest)
+    go m rest (j : js) = case lookup j (prefix rest) of
+      Just (pid, Left inv) -> case firstResp pid rest of
+        Just (k, resp) ->
           postcondition m inv resp
             && go (transition (transition m (Left inv)) (Right resp))
                   (dropFirstInv pid (filter ((/= k) . fst) rest)) js
-        [] -> False
+        Nothing -> False
       _ -> False
+    -- takeInvocations: the remaining events before the first remaining response
+    prefix = takeWhile (isInv . snd)
+    -- the roots of interleavings rest: prefix invocations whose pid has a response
+    roots rest = [ i | (i, (pid, Left _)) <- prefix rest, Just _ <- [firstResp pid rest] ]
+    firstResp pid rest = case [ (k, r) | (k, (q, Right r)) <- rest, q == pid ] of
+      kr : _ -> Just kr
+      []     -> Nothing
+    isInv (_, Left _) = True
+    isInv _           = False
     dropFirstInv pid evs = case break isInvOf evs of
       (before, _ : after) -> before ++ after
       (before, [])        -> before

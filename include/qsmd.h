@@ -238,7 +238,11 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *                       last finished call had no giant history)
  *   "wave_stats_ptr", "memo_stats_ptr", "memo_stats_groups"  diagnostics:
  *                       device buffers of per-workgroup / per-group records
- *                       (tools/wave_stats.py, tools/memo_stats.py) */
+ *                       (tools/wave_stats.py, tools/memo_stats.py)
+ *   "giant_stall_us"    diagnostic: the workgroup of the giant stage's first
+ *                       frontier chunk starts this late (tests of the time
+ *                       limit's phase-wait safety net: a giant combined by a
+ *                       workgroup that gave up waiting is BUDGET) */
 int qsmd_set_param(qsmd_ctx* ctx, const char* name, uint64_t value);
 
 /* Tuning knob (default 1024): histories the compact stages cannot hold go to

@@ -64,6 +64,7 @@ struct qsmd_ctx {
     uint64_t memo_stats_groups = 0;             // (memo_stats_groups)
     uint32_t memo_lds = 1;                      // heavy-stage memo tables in LDS: 0 never, 1 short lists, 2 always
     uint64_t giant_grid = 0;           // giant stage workgroups (0 = 2 per CU)
+    uint64_t giant_stall_us = 0;       // diagnostic: the giant stage's first frontier chunk starts this late
     // heavy stage: one wavefront per history (wave_search) unless the last
     // finished call sent more than wave_max histories there (then one lane
     // per history, memo_search); heavy_mode 0 / 1 forces wave / lane
@@ -297,6 +298,9 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "giant_grid") {
         if (value > 65536) return fail(c, QSMD_ERR_ARG, "giant_grid in 0..65536");
         c->giant_grid = value;
+    } else if (n == "giant_stall_us") {     // diagnostic (tests of the phase-wait safety net)
+        if (value > 10000000ull) return fail(c, QSMD_ERR_ARG, "giant_stall_us in 0..10^7");
+        c->giant_stall_us = value;
     } else if (n == "wave_min_rem") {
         c->wave_min_rem = std::min<uint64_t>(value, 0xFFFFFFFFull);
     } else if (n == "wave_stats_ptr") {     // diagnostic: device buffer of 8 x u64 per wave_search workgroup
@@ -589,6 +593,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     p.early = early ? 1u : 0u;
     p.totals = tot;
     p.probe_host = c->probe_host;
+    p.stall_ticks = c->giant_stall_us * 100ull;   // 100 MHz s_memrealtime
     if (flags & QSMD_FLAG_MEMO) {
         rc = memo_prepare(c, s, &p.memo);
         if (rc) return rc;

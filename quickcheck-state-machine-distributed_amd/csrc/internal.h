@@ -158,6 +158,7 @@ struct SplitArgs {
     qsmd_totals* totals;          // the call's totals (device), written by the last block
     uint32_t* probe_host;         // pinned host copy of counters [0..3] (null = none)
     uint32_t* debug;              // diagnostic: pinned host [grid][4] phase / progress (null = none)
+    uint64_t stall_ticks;         // diagnostic (giant_stall_us): the first frontier chunk starts this late
 };
 
 // Ordered fold of task results (reference DFS order); shared by the combine

@@ -356,13 +356,17 @@ __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32,
 }
 
 template <uint32_t MODEL, bool LT>
-static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s) {
+static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s,
+                                bool* lds_refused = nullptr) {
     const size_t lds = LT ? sizeof(MemoLds<MODEL, G32>) + (size_t)kLdsEntries * 8u * C_LANES * 4u
                           : (wide ? sizeof(MemoLds<MODEL, G64>) : sizeof(MemoLds<MODEL, G32>));
     if constexpr (LT) {   // beyond the default 64 KB of dynamic LDS (set on every launch: per device)
         const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&memo_search<MODEL, true>),
                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (attr != hipSuccess) return attr;
+        if (attr != hipSuccess) {
+            if (lds_refused) *lds_refused = true;
+            return attr;
+        }
     }
     hipLaunchKernelGGL((memo_search<MODEL, LT>), dim3(grid), dim3(C_LANES), lds, s, p32, p64, wide ? 1u : 0u);
     return hipGetLastError();
@@ -370,12 +374,18 @@ static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32
 
 hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool lds_tables,
                        hipStream_t s) {
-    const bool lt = lds_tables && !wide;
-    if (p32.s.model_id == QSMD_MODEL_BANK)
-        return lt ? launch_memo_t<QSMD_MODEL_BANK, true>(p32, p64, grid, wide, s)
-                  : launch_memo_t<QSMD_MODEL_BANK, false>(p32, p64, grid, wide, s);
-    return lt ? launch_memo_t<QSMD_MODEL_TICKET, true>(p32, p64, grid, wide, s)
-              : launch_memo_t<QSMD_MODEL_TICKET, false>(p32, p64, grid, wide, s);
+    const bool bank = p32.s.model_id == QSMD_MODEL_BANK;
+    if (lds_tables && !wide) {
+        bool refused = false;
+        const hipError_t e = bank ? launch_memo_t<QSMD_MODEL_BANK, true>(p32, p64, grid, wide, s, &refused)
+                                  : launch_memo_t<QSMD_MODEL_TICKET, true>(p32, p64, grid, wide, s, &refused);
+        if (!refused) return e;
+        // the device refused the LDS size (hipFuncSetAttribute): the HBM
+        // tables give the same results
+        (void)hipGetLastError();
+    }
+    return bank ? launch_memo_t<QSMD_MODEL_BANK, false>(p32, p64, grid, wide, s)
+                : launch_memo_t<QSMD_MODEL_TICKET, false>(p32, p64, grid, wide, s);
 }
 
 }  // namespace qsmd

@@ -746,12 +746,20 @@ __device__ uint32_t task_loop(const SplitArgs& p, uint32_t variant, GLds<MODEL, 
 // ----------------------------------------------------------------- combine
 
 // Fold giant g's tasks into its history's outputs; returns the status.
-__device__ int combine_one(const SplitArgs& p, uint32_t g, uint64_t& nodes) {
+// stale: a phase wait of this workgroup gave up (wait_for's safety net), so
+// the giant's frontier record or task results may be unfinished: BUDGET.
+__device__ int combine_one(const SplitArgs& p, uint32_t g, uint64_t& nodes, bool stale) {
     const SearchArgs& a = p.s;
-    const GiantRec G = p.giants[g];
-    const uint32_t h = G.h;
-    const uint64_t base = (uint64_t)G.variant * p.task_cap + G.first;
+    const uint32_t h = p.giant_list[g];
     nodes = 0;
+    if (stale) {
+        a.status[h] = QSMD_STATUS_BUDGET;
+        if (a.nodes) a.nodes[h] = a.max_nodes;
+        nodes = a.max_nodes;
+        return QSMD_STATUS_BUDGET;
+    }
+    const GiantRec G = p.giants[g];
+    const uint64_t base = (uint64_t)G.variant * p.task_cap + G.first;
     int64_t win = -1;
     const int st = combine_tasks(G.term_status, G.term_nodes, p.tasks + base, p.task_status + base,
                                  p.task_nodes + base, G.n_tasks, a.max_nodes, &nodes, &win);
@@ -792,15 +800,19 @@ __device__ __forceinline__ uint32_t poll_u32(const uint32_t* c) {
 
 // Wait until a phase counter reaches target (acquire).  A safety net bounds
 // the wait by twice the call's time limit (a stuck phase then reports
-// through timed_out instead of holding the GPU).
-__device__ __forceinline__ void wait_for(const uint32_t* ctr, uint32_t target, const SearchArgs& a, uint64_t t0) {
+// through timed_out instead of holding the GPU); returns true when it gave
+// up -- the phase before may still be running in another workgroup (one
+// that started late), so what this workgroup combines afterwards is BUDGET.
+__device__ __forceinline__ bool wait_for(const uint32_t* ctr, uint32_t target, const SearchArgs& a, uint64_t t0) {
     uint32_t polls = 0;
+    bool gave_up = false;
     while (poll_u32(ctr) < target) {
         __builtin_amdgcn_s_sleep(8);
         if ((++polls & 63u) == 0u) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // (and the L1 refreshed now and then)
             if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > 2 * a.time_limit) {
                 atomicOr(a.timed_out, 2u);
+                gave_up = true;
                 break;
             }
         }
@@ -808,6 +820,7 @@ __device__ __forceinline__ void wait_for(const uint32_t* ctr, uint32_t target, c
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    return gave_up;
 }
 
 __device__ __forceinline__ uint32_t ld_cnt(const uint32_t* c) { return poll_u32(c); }
@@ -877,6 +890,9 @@ __global__ __launch_bounds__(64) void giant_search(SplitArgs p) {
         if (lane == 0) c0 = atomicAdd(cnt + C_GNEXT, 64u);
         c0 = __shfl(c0, 0, 64);
         if (c0 >= n_g) break;
+        if (p.stall_ticks && c0 == 0u) {        // diagnostic: the first chunk's workgroup starts late
+            while (__builtin_amdgcn_s_memrealtime() - t0 < p.stall_ticks) __builtin_amdgcn_s_sleep(127);
+        }
         const uint32_t g = c0 + (uint32_t)lane;
         const bool in = g < n_g;
         uint32_t h = 0;
@@ -898,7 +914,7 @@ __global__ __launch_bounds__(64) void giant_search(SplitArgs p) {
     }
     beat(p, lane, 0, 2);
     // ---- tasks (every frontier done: the task lists are complete)
-    wait_for(cnt + C_GDONE, n_g, a, t0);
+    bool stale = wait_for(cnt + C_GDONE, n_g, a, t0);
     beat(p, lane, 0, 3);
     uint32_t took = task_loop<MODEL, uint64_t, 64, 8, 64>(p, 0u, u.v0, lane, t0, cnt + C_TQ0);
     __syncthreads();
@@ -912,7 +928,7 @@ __global__ __launch_bounds__(64) void giant_search(SplitArgs p) {
     beat(p, lane, 2, took);
     // ---- combine (every task done)
     const uint32_t n_tasks = min(ld_cnt(cnt + C_TASKS0), p.task_cap) + min(ld_cnt(cnt + C_TASKS1), p.task_cap);
-    wait_for(cnt + C_TDONE, n_tasks, a, t0);
+    stale |= wait_for(cnt + C_TDONE, n_tasks, a, t0);
     beat(p, lane, 0, 5);
     Counters cc;
     for (;;) {
@@ -923,7 +939,7 @@ __global__ __launch_bounds__(64) void giant_search(SplitArgs p) {
         const uint32_t g = c0 + (uint32_t)lane;
         if (g < n_g) {
             uint64_t nodes = 0;
-            const int st = combine_one(p, g, nodes);
+            const int st = combine_one(p, g, nodes, stale);
             cc.add(st, nodes);
         }
         publish_add(cnt + C_CDONE, min(64u, n_g - c0), lane);
@@ -932,7 +948,7 @@ __global__ __launch_bounds__(64) void giant_search(SplitArgs p) {
     // ---- early exit: every history after the first failing one is SKIPPED,
     // and the totals are recounted from the final outputs
     if (p.early) {
-        wait_for(cnt + C_CDONE, n_g, a, t0);
+        (void)wait_for(cnt + C_CDONE, n_g, a, t0);
         const uint32_t ff = ld_cnt(a.first_fail);
         Counters xc;
         uint64_t skipped = 0;

@@ -103,11 +103,28 @@ def _allreduce(arr, op, group=None):
     import torch
     import torch.distributed as dist
 
-    t = torch.as_tensor(np.ascontiguousarray(arr, dtype=np.int64))
+    t = torch.tensor(np.asarray(arr, dtype=np.int64))        # a copy: gloo reduces in place
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         t = t.to(_collective_device(group))
         dist.all_reduce(t, op=op, group=group)
     return t.cpu().numpy().astype(np.int64)
+
+
+def round_windows(n, world, round_tasks=None, first_per_rank=2):
+    """The task windows [c0, c1) of check_single_split's rounds: a fixed
+    window of ``round_tasks`` tasks, or by default a geometric schedule --
+    ``first_per_rank`` tasks per rank in the first round, doubling every
+    round -- so an early deciding task (the first subtree of a linearisable
+    history usually holds its witness) stops every rank after a few tasks,
+    while an exhausted history still takes only ~log2(n / world) rounds."""
+    out, c0 = [], 0
+    w = round_tasks or max(1, first_per_rank) * world
+    while c0 < n:
+        out.append((c0, min(n, c0 + w)))
+        c0 += w
+        if not round_tasks:
+            w *= 2
+    return out
 
 
 def check_single_split(checker, model_id, hdr, events, rank, world, model0=None, flags=1,
@@ -117,12 +134,14 @@ def check_single_split(checker, model_id, hdr, events, rank, world, model0=None,
     Each rank cuts the search at the same frontier (checker.split_frontier
     is deterministic), so no task list is exchanged; rank r searches the
     tasks t = r, r + world, ... (round-robin in DFS order).  Work goes in
-    rounds over windows of the task list; after each round one MIN
-    all-reduce publishes the first task found deciding (True or Map.!), and
-    no rank searches a task after it -- every task before it has been
-    searched in full by its owner, so the node count stays exact.  Then one
-    SUM all-reduce gathers the per-task results (each rank contributes only
-    its own entries) and every rank folds them in DFS order.
+    rounds over windows of the task list (round_windows: geometric by
+    default, or ``round_tasks`` per round); after each round one MIN
+    all-reduce publishes the first task found deciding (True or Map.!) --
+    the early-termination flag of §8e -- and no rank searches a task after
+    it: every task before it has been searched in full by its owner, so the
+    node count stays exact.  Then one SUM all-reduce gathers the per-task
+    results (each rank contributes only its own entries) and every rank
+    folds them in DFS order.
 
     checker: qsmd.device.Context (or anything with split_frontier /
     check_tasks).  Returns (status, nodes, witness path or None, info dict).
@@ -139,11 +158,10 @@ def check_single_split(checker, model_id, hdr, events, rank, world, model0=None,
     st_local = np.zeros(n, dtype=np.int64)           # status + 1 where searched here
     nd_local = np.zeros(n, dtype=np.int64)
     rows = {}
-    window = round_tasks or max(world, n)
     best = _NO_TASK
     rounds = 0
-    for c0 in range(0, n, window):
-        sel = np.arange(c0 + rank, min(c0 + window, n), world)
+    for c0, c1 in round_windows(n, world, round_tasks):
+        sel = np.arange(c0 + (rank - c0) % world, c1, world)     # this rank's tasks t = rank (mod world)
         sel = sel[sel < best]
         if len(sel):
             s, nd, w = checker.check_tasks(model_id, hdr, events, tasks[sel], model0, flags, max_nodes,

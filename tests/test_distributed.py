@@ -146,15 +146,16 @@ def _split_worker(rank, world, port, round_tasks, out_q):
             st, nodes, w, info = qdist.check_single_split(split_emu.EmuChecker(), mid, h, e, rank, world,
                                                           tasks_per_rank=8, round_tasks=round_tasks)
             res.append((int(st), int(nodes), None if w is None else [int(x) for x in w],
-                        info["searched_here"]))
+                        info["searched_here"], info["rounds"], info["n_tasks"], info["winner"]))
         out_q.put((rank, res))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("round_tasks", [4, None])
+@pytest.mark.parametrize("round_tasks", [4, None, 10**9])
 def test_two_rank_gloo_single_history_split(round_tasks):
     import oracle_c
+    from qsmd import dist as qdist
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -169,9 +170,29 @@ def test_two_rank_gloo_single_history_split(round_tasks):
     for j, (mid, h, e) in enumerate(_heavy_histories(3)):
         st_o, nd_o, w_o = oracle_c.check_batch(mid, h, e, witness=True)
         for r in range(world):
-            st, nodes, w, _ = results[r][j]
+            st, nodes, w = results[r][j][:3]
             assert (st, nodes) == (int(st_o[0]), int(nd_o[0]))
             if st == 1:
                 assert w == [int(x) for x in w_o[:len(w)]] and (len(w) == len(w_o) or w_o[len(w)] == 0xFF)
         if int(nd_o[0]) > 1000:          # split into tasks, and the ranks shared them
             assert results[0][j][3] > 0 and results[1][j][3] > 0
+        n_tasks, win, searched = results[0][j][5], results[0][j][6], results[0][j][3] + results[1][j][3]
+        if round_tasks == 10**9:
+            assert results[0][j][4] == min(n_tasks, 1) and searched == n_tasks   # one round: every task searched
+        elif win >= 0:
+            # the first deciding task stops both ranks at the end of its round
+            windows = qdist.round_windows(n_tasks, world, round_tasks)
+            k = next(i for i, (c0, c1) in enumerate(windows) if c0 <= win < c1)
+            assert results[0][j][4] == k + 1 and searched <= windows[k][1]
+
+
+def test_round_windows():
+    from qsmd import dist as qdist
+    assert qdist.round_windows(100, 2) == [(0, 4), (4, 12), (12, 28), (28, 60), (60, 100)]
+    assert qdist.round_windows(10, 3, 4) == [(0, 4), (4, 8), (8, 10)]
+    assert qdist.round_windows(0, 8) == []
+    for n in range(0, 200, 7):
+        for world in (1, 2, 3, 8):
+            w = qdist.round_windows(n, world)
+            assert (w[0][0] if w else 0) == 0 and (w[-1][1] if w else n) == n
+            assert all(a[1] == b[0] for a, b in zip(w, w[1:]))

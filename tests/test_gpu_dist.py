@@ -75,6 +75,14 @@ def _worker(rank, world, port, n_total, out_q):
                                                          flags=device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_MEMO)
             splits.append((int(s), int(nodes), None if w is None else [int(x) for x in w], info["searched_here"]))
         res["split"] = splits
+        # the linearisable 8 x 64 history once more in ONE round over every
+        # task (no cross-rank early exit): the same verdict, more tasks searched
+        h, e, _ = gen.adversarial_ticket(8, 64, bug=False)
+        s, nodes, w, info = qdist.check_single_split(ctx, 1, h, e, rank, world, tasks_per_rank=16,
+                                                     round_tasks=10**9,
+                                                     flags=device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_MEMO)
+        res["one_round"] = (int(s), None if w is None else [int(x) for x in w], info["searched_here"],
+                            info["n_tasks"], info["rounds"])
         out_q.put((rank, res))
     finally:
         ctx.close()
@@ -125,3 +133,12 @@ def test_two_processes_on_the_hip_kernels():
             assert s == int(s_o[0]) == (0 if bug else 1)
             if not bug:
                 assert w == [int(x) for x in w_o[:len(w)]]
+    # cross-rank early exit (§8e): the geometric rounds stop both ranks at
+    # the first deciding task; one round over all tasks searches them all
+    early = sum(results[r]["split"][4][3] for r in range(world))
+    full = sum(results[r]["one_round"][2] for r in range(world))
+    for r in range(world):
+        assert results[r]["one_round"][0] == results[r]["split"][4][0] == 1
+        assert results[r]["one_round"][1] == results[r]["split"][4][2]
+        assert results[r]["one_round"][4] == 1
+    assert results[0]["one_round"][3] > 2 * world and early < full, (early, full)

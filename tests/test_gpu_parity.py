@@ -444,32 +444,56 @@ def test_encode_errors(ctx):
     assert tot["encode_errors"] == 4
 
 
-def test_device_resident_full_size(ctx):
-    """BASELINE config 2 at full size (1M histories) through the device entry
-    point: size-independent properties (all linearisable by construction,
-    totals == sums) and the oracle's verdict and node count for every
-    history."""
+# BASELINE.json configs at their single-GPU sizes: config 1 (TicketDispenser
+# 2 x 10), config 2 (Bank 4 x 16, 1M: the headline), config 3 (Bank with
+# injected bugs: 10M over 8 GPUs, i.e. 1.25M per GPU; 1M here), config 5
+# (Bank 6 x 24, 100k, exhaustive).  Config 4 (one adversarial history) is
+# tests/test_gpu_split.py::test_adversarial_ticket_memo.
+FULL_SIZE = [("ticket_2x10", 1_000_000), ("bank_4x16", 1_000_000), ("bank_4x16_bugs", 1_000_000),
+             ("bank_6x24", 100_000)]
+
+
+@pytest.mark.parametrize("name,n", FULL_SIZE)
+def test_device_resident_full_size(ctx, name, n):
+    """Every generated BASELINE config at full single-GPU size through the
+    device entry point (inputs resident in HBM, as bench.py runs them): the
+    oracle's verdict and node count for every history, the witness of every
+    linearisable one, and the totals; plus the size-independent properties
+    (Bank without bugs: all linearisable by construction)."""
     torch = pytest.importorskip("torch")
-    n = 1_000_000
-    hdr, ev, bug = gen.generate_config("bank_4x16", 0, n)
+    mid = gen.CONFIGS[name]["model_id"]
+    hdr, ev, bug = gen.generate_config(name, 0, n)
     dev = torch.device("cuda:0")
     d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
     d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
     d_st = torch.empty(n, dtype=torch.uint8, device=dev)
     d_nd = torch.empty(n, dtype=torch.int64, device=dev)
+    d_w = torch.full((len(ev),), 0xFF, dtype=torch.uint8, device=dev)
     d_tot = torch.zeros(8, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
-    ctx.check_device(models.MODEL_BANK, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev),
-                     d_st.data_ptr(), d_nd.data_ptr(), None, d_tot.data_ptr(), stream=stream)
+    ctx.check_device(mid, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st.data_ptr(), d_nd.data_ptr(),
+                     d_w.data_ptr(), d_tot.data_ptr(), flags=device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_WITNESS,
+                     max_nodes=10**7, stream=stream)
     torch.cuda.synchronize()
     st = d_st.cpu().numpy()
     nd = d_nd.cpu().numpy().astype(np.uint64)
+    w = d_w.cpu().numpy()
     tot = d_tot.cpu().numpy()
-    assert (st == codec.STATUS_LIN).all()
-    assert int(tot[0]) == n and int(tot[1]) == n and int(tot[7]) == int(nd.sum())
-    assert (nd >= 16).all()
-    st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr, ev, threads=8)
-    assert np.array_equal(st_o, st) and np.array_equal(nd_o, nd)
+    st_o, nd_o, w_o = oracle_c.check_batch(mid, hdr, ev, max_nodes=10**7, threads=16, witness=True)
+    bad = np.nonzero((st != st_o) | (nd != nd_o))[0]
+    assert len(bad) == 0, f"{len(bad)} mismatches, first {bad[:5]}: dev {st[bad[:5]]}/{nd[bad[:5]]} " \
+                          f"oracle {st_o[bad[:5]]}/{nd_o[bad[:5]]}"
+    lin = st == codec.STATUS_LIN
+    n_ev = hdr["n_ev"].astype(np.int64)
+    assert hdr["ev_off"][0] == 0 and np.array_equal(np.cumsum(n_ev)[:-1], hdr["ev_off"][1:].astype(np.int64))
+    mask = np.repeat(lin, n_ev)                                # the events of linearisable histories
+    assert np.array_equal(w[mask], w_o[mask]), "witness mismatch"
+    assert int(tot[0]) == int((st <= 2).sum()) and int(tot[1]) == int(lin.sum())
+    assert int(tot[2]) == int((st == 0).sum()) and int(tot[7]) == int(nd.sum())
+    if name in ("bank_4x16", "bank_6x24"):
+        assert lin.all()
+    if name == "bank_4x16_bugs":
+        assert (st == codec.STATUS_NONLIN).sum() > n // 10   # the early-termination path is exercised
 
 
 @pytest.mark.parametrize("packed", [True, False])

@@ -270,3 +270,32 @@ def test_time_limit_is_reported(ctx):
     st, nd, _, _ = ctx.check_arrays(models.MODEL_TICKET, h2, e2)
     assert (int(st[0]), int(nd[0])) == (codec.STATUS_NONLIN, 923201)
     assert not ctx.timed_out()
+
+
+def test_stalled_giant_workgroup_reports_budget(ctx):
+    """The giant stage's phase waits give up after twice the time limit
+    (wait_for's safety net).  A workgroup that gave up may meet frontier
+    records and task results another workgroup has not finished (one that
+    started late), or that an earlier call left in the reused workspace: the
+    giants it combines are BUDGET, never a stale verdict.  Forced here with
+    the diagnostic stall of the first frontier chunk's workgroup."""
+    hdr, ev, _ = gen.generate_config("ticket_8x64", 0, 400)
+    first = (hdr[:200].copy(), ev)
+    second = (hdr[200:].copy(), ev)
+    st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_TICKET, second[0], second[1], threads=8, max_nodes=10**7)
+    ctx.check_arrays(models.MODEL_TICKET, *first, max_nodes=10**7)      # records of another batch
+    ctx.set_time_limit_ms(5)
+    ctx.set_param("giant_stall_us", 100000)
+    try:
+        st, nd, _, tot = ctx.check_arrays(models.MODEL_TICKET, *second, max_nodes=10**7)
+        assert ctx.timed_out()
+    finally:
+        ctx.set_param("giant_stall_us", 0)
+        ctx.set_time_limit_ms(60000)
+    budget = st == codec.STATUS_BUDGET
+    assert budget.sum() > 0
+    ok = ~budget
+    assert np.array_equal(st[ok], st_o[ok]) and np.array_equal(nd[ok], nd_o[ok])
+    assert tot["budget"] == int(budget.sum())
+    # the context is sound afterwards
+    _compare(ctx, models.MODEL_TICKET, second[0], second[1], max_nodes=10**7)

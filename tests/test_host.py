@@ -178,6 +178,87 @@ def test_replay_witness_accepts_oracle_witnesses_and_rejects_others():
     assert checked > 50
 
 
+def _ll_closures(model):
+    if model == "ticket":
+        return LL.ticket_transition, LL.ticket_postcondition, None
+    return LL.bank_next, LL.bank_post, {}
+
+
+def test_haskell_replay_accepts_exactly_the_reference_paths():
+    """The Haskell drop-in re-checks every device True with `replay`
+    (hs/Linearisability/Device.hs); its Python mirror (tests/hs_replay.py)
+    accepts exactly the successful root-to-leaf paths of the reference's
+    tree, and rejects truncated witnesses and invocations chosen after a
+    pending response (outside takeInvocations, src/Linearisability.hs:25-28)."""
+    from hs_replay import hs_replay, successful_paths
+    rng = random.Random(31)
+    n_paths = n_trunc = n_outside = 0
+
+    def lin_ticket(n_ops, n_pid):
+        # each operation takes effect at its response: always linearisable,
+        # often in several orders
+        pids = [f"p{i}" for i in range(n_pid)]
+        h, pend, n, left = [("p0", ("L", "Reset")), ("p0", ("R", "Ok"))], {}, 0, n_ops
+        while left or pend:
+            p = rng.choice(pids)
+            if p not in pend and left:
+                pend[p] = rng.choice(["TakeTicket", "TakeTicket", "Reset"])
+                h.append((p, ("L", pend[p])))
+                left -= 1
+            elif p in pend:
+                inv = pend.pop(p)
+                n = n + 1 if inv == "TakeTicket" else 0
+                h.append((p, ("R", ("Number", n) if inv == "TakeTicket" else "Ok")))
+        return h
+
+    for it in range(400):
+        model = rng.choice(["ticket", "bank"])
+        if it % 2:
+            model, hist = "ticket", lin_ticket(rng.randint(1, 5), rng.randint(1, 3))
+        else:
+            hist = histgen.wellformed_history(rng, model, rng.randint(1, 5), rng.randint(1, 3))
+        tr, post, m0 = _ll_closures(model)
+
+        def rep(ws, hist=hist, tr=tr, post=post, m0=m0):
+            try:
+                return hs_replay(tr, post, m0, hist, ws)
+            except LL.ModelError:
+                return False
+        paths = successful_paths(tr, post, m0, hist)
+        good = {tuple(p) for p in paths}
+        for p in paths:
+            assert rep(p), (hist, p)
+            n_paths += 1
+            for k in range(len(p)):                        # every truncation
+                if tuple(p[:k]) not in good:
+                    assert not rep(p[:k]), (hist, p[:k])
+                    n_trunc += 1
+        # random index sequences: accepted iff a successful path
+        inv_idx = [i for i, (_, ev) in enumerate(hist) if ev[0] == "L"]
+        for _ in range(20):
+            ws = [rng.choice(inv_idx) for _ in range(rng.randint(1, len(inv_idx)))] if inv_idx else []
+            assert rep(ws) == (tuple(ws) in good or (not ws and not hist)), (hist, ws)
+        # an invocation after the first remaining response is never a root
+        first_r = next((i for i, (_, ev) in enumerate(hist) if ev[0] == "R"), None)
+        late = [i for i in inv_idx if first_r is not None and i > first_r]
+        for j in late:
+            assert not rep([j]), (hist, j)
+            n_outside += 1
+        # the Python host replay agrees with the Haskell one on the paths
+        m = models.BY_NAME[model]
+        for p in paths[:3]:
+            assert replay_witness(m, hist, p)
+    assert n_paths > 100 and n_trunc > 50 and n_outside > 50, (n_paths, n_trunc, n_outside)
+    # KAT-7 by hand: `Open b` (event 2) lies after a's pending response
+    # (event 1), so it cannot come first; `Open a` alone is not a leaf
+    _, h7, _, _ = KATS["KAT7_bank_concurrent"]
+    assert not hs_replay(LL.bank_next, LL.bank_post, {}, h7, [2])          # Open b before a's response
+    assert not hs_replay(LL.bank_next, LL.bank_post, {}, h7, [0])          # truncated: Open a only
+    src = open(os.path.join(ROOT, "hs", "Linearisability", "Device.hs")).read()
+    assert "lookup j (prefix rest)" in src and "go _ rest [] = null (roots rest)" in src
+    assert "replay _ _ _ hist [] = null hist" in src
+
+
 def test_combine_tasks_host():
     """qsmd_combine_tasks (host code of the C ABI): the reference count is
     the nodes above the cut up to the deciding task + every earlier subtree."""
