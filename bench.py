@@ -158,6 +158,23 @@ class InFlight:
             elapsed = float(e.item())
         return elapsed
 
+    def roofline_leg(self, calls):
+        """The dominant kernel alone: `calls` synchronous calls on slot 0 (each
+        waits for the previous, nothing else on the GPU), with the stage-0
+        HIP events on the launch stream -- the per-launch time the roofline
+        divides by, and the launches a kernel trace of this command shows last
+        (profiles/summarize_pmc.py --last)."""
+        torch.cuda.synchronize(self.dev)
+        self.ctxs[0].timing_reset()
+        d_st, d_nd = self.outs[0]
+        for _ in range(calls):
+            self.ctxs[0].check_device(self.model_id, self.d_hdr.data_ptr(), self.n, self.d_ev.data_ptr(), self.n_ev,
+                                      d_st.data_ptr(), d_nd.data_ptr(), None, None, flags=self.flags,
+                                      stream=self.streams[0].cuda_stream)
+            torch.cuda.synchronize(self.dev)
+        s0, call = self.ctxs[0].timing_read()
+        return np.asarray(s0, dtype=np.float64), np.asarray(call, dtype=np.float64)
+
     def results(self):
         i, row, par = self.last
         st = self.outs[i][0].cpu().numpy()
@@ -288,8 +305,10 @@ def main():
                     help="rounds of in-flight steps whose counters one RCCL all-reduce carries (N > 1)")
     ap.add_argument("--device-gen", action="store_true",
                     help="generate the batch on the GPU (qsmd_gen_batch_device; same histories as the host generator)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r02", "stage0_pmc.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03", "stage0_pmc.json"),
                     help="PMC summary of the stage-0 kernel (profiles/summarize_pmc.py) for the roofline fields")
+    ap.add_argument("--roof-calls", type=int, default=30,
+                    help="synchronous calls after the timed region that time the dominant kernel alone")
     args = ap.parse_args()
 
     # stdout carries exactly one JSON line (rank 0): RCCL prints a version
@@ -382,6 +401,7 @@ def main():
     elapsed = run.timed(args.steps, args.warmup)
     s0_ms, call_ms = run.ctxs[0].timing_read()
     st, nd, tot = run.results()
+    roof_s0, roof_call = run.roofline_leg(max(1, args.roof_calls))
     run.close()
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -390,17 +410,26 @@ def main():
     nodes_total = int(tot[7])
     assert int(tot[0]) + int(tot[4]) + int(tot[5]) == total_hist, tot
 
-    # roofline of the dominant kernel (stage 0), rank-local: algorithmic bytes
-    #  over its live HIP-event time; beside it the fractions the
-    # PMC counters of a profiling run of the same configuration give for the
-    # same live time: HBM bytes actually moved, and VALU issue
-    s0_mean = float(np.mean(s0_ms)) if len(s0_ms) else float("nan")
-    t_s0 = s0_mean * 1e-3
+    # roofline of the dominant kernel (stage 0), rank-local: SURVEY §8d
+    # algorithmic bytes of one launch over its mean duration ALONE on the GPU
+    # (the roofline leg: synchronous calls after the timed region, HIP events
+    # on the launch stream; a kernel trace of this command shows the same
+    # launches last).  Beside it: the same bytes per step of the timed
+    # region, and what the PMC counters of a profiled run of the same
+    # configuration give for the same launches (HBM bytes moved, VALU issue).
+    t_s0 = float(np.mean(roof_s0)) * 1e-3
     a_bytes = alg_bytes(hdr, np.minimum(nd, budget0) if budget0 > 0 else nd)
     achieved = a_bytes / t_s0 / 1e9
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": a_bytes,
-            "hbm_io_bytes_per_launch": hbm_bytes(hdr), "kernel": "compact_search<Bank, G32> (stage 0)"}
+            "hbm_io_bytes_per_launch": hbm_bytes(hdr), "kernel": "compact_search<Bank, G32> (stage 0)",
+            "kernel_ms": {"mean": float(np.mean(roof_s0)), "median": float(np.median(roof_s0)),
+                          "min": float(np.min(roof_s0)), "launches": int(len(roof_s0)),
+                          "call_mean": float(np.mean(roof_call)), "call_median": float(np.median(roof_call)),
+                          "how": "synchronous calls after the timed region, HIP events around stage 0"},
+            "per_step": {"achieved": a_bytes / (ms_per_step * 1e-3) / 1e9,
+                         "frac": a_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "how": "algorithmic bytes of one launch / ms_per_step (calls in flight)"}}
     if os.path.exists(args.pmc):
         with open(args.pmc) as f:
             pmc = json.load(f)
@@ -431,7 +460,9 @@ def main():
         "verdicts": {"checked": int(tot[0]), "linearisable": int(tot[1]),
                      "nonlinearisable": int(tot[2]), "model_errors": int(tot[3]),
                      "budget": int(tot[5])},
-        "device_ms": {"stage0_mean": s0_mean, "call_mean": float(np.mean(call_ms)) if len(call_ms) else None},
+        "device_ms": {"in_flight": {"stage0_mean": float(np.mean(s0_ms)) if len(s0_ms) else None,
+                                    "call_mean": float(np.mean(call_ms)) if len(call_ms) else None},
+                      "alone": {"stage0_mean": float(np.mean(roof_s0)), "call_mean": float(np.mean(roof_call))}},
         "roofline": roof,
         "cpu_baseline": None,
     }

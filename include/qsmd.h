@@ -216,29 +216,31 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *   "stage0_grid"       as qsmd_set_stage0_grid
  *   "split_budget"      as qsmd_set_split_budget
  *   "split_xmemo"       1 (default): the giant stage's exact-count memo
- *   "heavy_mode"        1 (default): one lane per heavy history with a
- *                       private memo table; 0: one wavefront per heavy
- *                       history; 2: lane mode while the last finished call
- *                       sent more than "wave_max" (default 16384) histories
- *                       to the heavy stage, else wave mode
+ *   "heavy_mode"        2 (default): the heavy stage in wave mode (one
+ *                       wavefront per history, the DFS in wave-uniform
+ *                       registers, an LDS memo per wavefront) unless the last
+ *                       finished call sent more than "wave_max" (default
+ *                       16384) histories there, then lane mode (one lane per
+ *                       history, a private memo table per lane); 0: always
+ *                       wave mode; 1: always lane mode
  *   "memo_lds"          lane mode's memo tables: 1 (default) in LDS when the
  *                       last finished call's heavy histories fit one
- *                       workgroup per CU (fastest for one call at a time),
- *                       else in HBM; 0: always HBM (better with several
- *                       calls in flight: an LDS-table workgroup holds a CU);
- *                       2: always LDS
- *   "memo_grid", "memo_lane_entries"  lane mode: workgroups, entries per lane
- *                       (HBM; the LDS tables hold min(64, entries))
- *   "wave_budget"       wave mode: nodes a lane's task counts before it may
- *                       hand the rest to idle lanes (default 16)
- *   "wave_grid"         wave mode workgroups (0 = 3 per CU)
- *   "wave_min_rem"      wave mode: no memo probe below this many remaining
- *                       events
+ *                       workgroup per CU, else in HBM; 0: always HBM (an
+ *                       LDS-table workgroup holds a CU); 2: always LDS
+ *   "memo_grid", "memo_lane_entries"  lane mode: workgroups at most (0 = 12
+ *                       per CU), entries per lane (HBM tables: grid x 64 x
+ *                       entries x 96 B, grown on demand; the LDS tables hold
+ *                       min(64, entries))
+ *   "wave_grid"         wave mode workgroups (0 = the last call's heavy count
+ *                       + 25 %, at most 16 per CU; grid-stride beyond)
+ *   "wave_min_rem"      wave mode: no memo probe at nodes with at most this
+ *                       many remaining events (default 4)
  *   "giant_grid"        giant stage workgroups (0 = 2 per CU, or 64 when the
  *                       last finished call had no giant history)
  *   "wave_stats_ptr", "memo_stats_ptr", "memo_stats_groups"  diagnostics:
- *                       device buffers of per-workgroup / per-group records
- *                       (tools/wave_stats.py, tools/memo_stats.py)
+ *                       device buffers: wave mode [max, sum] of DFS
+ *                       iterations per history (tools/wave_stats.py), lane
+ *                       mode per-group records (tools/memo_stats.py)
  *   "giant_stall_us"    diagnostic: the workgroup of the giant stage's first
  *                       frontier chunk starts this late (tests of the time
  *                       limit's phase-wait safety net: a giant combined by a

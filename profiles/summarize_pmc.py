@@ -1,17 +1,24 @@
-"""Summarise a profiles/profile.sh run: per-kernel mean duration (kernel
-trace) and per-dispatch PMC counters of the dominant search kernel.
+"""Summarise a profiles/profile.sh run: per-dispatch durations (kernel trace)
+and PMC counters of the dominant search kernel (stage 0), over the LAST
+`--last` dispatches of that kernel -- bench.py's roofline leg, the
+synchronous calls it times after its timed region -- so that the profile's
+mean duration is the one bench.py's `roofline.kernel_ms.mean` divides by.
+The whole-run rocprofv3 --stats table is kept beside it (`kernels`).
 
 HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are
 collected in separate passes, are in KiB, and on gfx950 FETCH_SIZE reports
 half the bytes of a wide coalesced read, so traffic = (2*FETCH_SIZE +
 WRITE_SIZE) * 1024 per dispatch (the uncorrected value is reported too).
+
+    python3 profiles/summarize_pmc.py <out_dir> [--last 30]
 """
 
+import argparse
 import csv
 import glob
 import json
 import os
-import sys
+import statistics
 from collections import defaultdict
 
 DOMINANT = "compact_search"
@@ -20,44 +27,70 @@ GEOMETRY = "G32>"            # stage 0 (stage 0w is the G64 instance)
 
 def rows(path_glob):
     out = []
-    for p in glob.glob(path_glob, recursive=True):
+    for p in sorted(glob.glob(path_glob, recursive=True)):
         with open(p) as f:
             out.extend(csv.DictReader(f))
     return out
 
 
-def counters(out_dir, name):
+def is_dominant(name):
+    return DOMINANT in name and GEOMETRY in name
+
+
+def dispatch_key(r):
+    d = r.get("Dispatch_Id") or r.get("Correlation_Id") or "0"
+    return int(d)
+
+
+def durations(out_dir, last):
+    """Durations (ns) of the dominant kernel's dispatches, in dispatch order."""
+    tr = [r for r in rows(os.path.join(out_dir, "trace", "**", "*kernel_trace.csv")) if is_dominant(r["Kernel_Name"])]
+    tr.sort(key=dispatch_key)
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr]
+    return d, d[-last:] if last else d
+
+
+def counters(out_dir, name, last):
     per = defaultdict(lambda: defaultdict(float))   # dispatch -> counter -> value
-    kname = {}
     for r in rows(os.path.join(out_dir, name, "**", "*counter_collection.csv")):
-        k = r.get("Kernel_Name", "")
-        if DOMINANT not in k or GEOMETRY not in k:
+        if not is_dominant(r.get("Kernel_Name", "")):
             continue
-        d = r.get("Dispatch_Id") or r.get("Correlation_Id")
-        per[d][r["Counter_Name"]] += float(r["Counter_Value"])
-        kname[d] = k
+        per[dispatch_key(r)][r["Counter_Name"]] += float(r["Counter_Value"])
     if not per:
-        return {}
-    names = set(c for v in per.values() for c in v)
-    return {c: sum(v.get(c, 0.0) for v in per.values()) / len(per) for c in names}
+        return {}, 0
+    keys = sorted(per)[-last:] if last else sorted(per)
+    names = set(c for k in keys for c in per[k])
+    return {c: sum(per[k].get(c, 0.0) for k in keys) / len(keys) for c in names}, len(keys)
 
 
-def main(out_dir):
-    res = {"dominant_kernel": DOMINANT}
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out_dir", nargs="?", default="gpurun_out/prof")
+    ap.add_argument("--last", type=int, default=30, help="dispatches of the dominant kernel to summarise (0 = all)")
+    args = ap.parse_args()
+    out_dir = args.out_dir
+    res = {"dominant_kernel": f"{DOMINANT}<..., {GEOMETRY[:-1]}> (stage 0)", "last_dispatches": args.last}
     stats = rows(os.path.join(out_dir, "trace", "**", "*kernel_stats.csv"))
     res["kernels"] = {r["Name"]: {"calls": int(r["Calls"]), "mean_ns": float(r["AverageNs"]),
                                   "pct": float(r["Percentage"])} for r in stats}
-    dur = [v["mean_ns"] for k, v in res["kernels"].items() if DOMINANT in k and GEOMETRY in k]
-    res["dominant_mean_ns"] = dur[0] if dur else None
-    f = counters(out_dir, "fetch").get("FETCH_SIZE")
-    w = counters(out_dir, "write").get("WRITE_SIZE")
+    all_d, d = durations(out_dir, args.last)
+    if d:
+        res["dominant"] = {"dispatches": len(d), "mean_ns": statistics.mean(d), "median_ns": statistics.median(d),
+                           "min_ns": min(d), "max_ns": max(d), "all_dispatches": len(all_d),
+                           "all_mean_ns": statistics.mean(all_d)}
+        res["dominant_mean_ns"] = statistics.mean(d)
+    f, nf = counters(out_dir, "fetch", args.last)
+    w, nw = counters(out_dir, "write", args.last)
+    f, w = f.get("FETCH_SIZE"), w.get("WRITE_SIZE")
     res["FETCH_SIZE_kib"] = f
     res["WRITE_SIZE_kib"] = w
+    res["pmc_dispatches"] = {"fetch": nf, "write": nw}
     if f is not None and w is not None:
         res["hbm_bytes_per_launch"] = (2.0 * f + w) * 1024.0
         res["hbm_bytes_per_launch_uncorrected"] = (f + w) * 1024.0
-    sq = counters(out_dir, "sq1")
-    sq.update(counters(out_dir, "sq2"))
+    sq, _ = counters(out_dir, "sq1", args.last)
+    sq2, _ = counters(out_dir, "sq2", args.last)
+    sq.update(sq2)
     res["sq"] = sq
     res["valu_insts_per_launch"] = sq.get("SQ_INSTS_VALU")
     res["lds_bank_conflict_cycles"] = sq.get("SQ_LDS_BANK_CONFLICT")
@@ -72,10 +105,15 @@ def main(out_dir):
             b = json.loads(fjs.read().strip().splitlines()[-1])
         res["config"] = b["config"]["workload"]
         res["n_hist"] = b["config"]["histories_per_gpu"]
+        res["bench_kernel_ms"] = b["roofline"].get("kernel_ms")
+        res["bench_frac"] = b["roofline"]["frac"]
+        res["bench_alg_bytes_per_launch"] = b["roofline"]["alg_bytes_per_launch"]
+        if d:
+            res["frac_from_profile"] = b["roofline"]["alg_bytes_per_launch"] / (res["dominant_mean_ns"] * 1e-9) / 8e12
     except Exception:
         pass
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof")
+    main()

@@ -56,30 +56,28 @@ struct qsmd_ctx {
     uint64_t stage0_budget = 32;       // stage-0 node budget before the heavy stage
     uint64_t stage0w_budget = 32;      // stage-0w node budget before the heavy stage
     uint64_t split_budget = 1024;      // giant stage: whole-search iterations = 16x, heavy-stage cap = 64x
-    uint64_t wave_budget = 16;         // heavy stage: nodes a task searches before it may split
-    uint64_t wave_grid = 0;            // heavy stage workgroups (0 = 3 per CU)
-    uint64_t wave_min_rem = 8;         // heavy stage: nodes with at most this many events left skip the memo
-    unsigned long long* wave_stats = nullptr;   // diagnostic (wave_stats_ptr): 8 x u64 per workgroup
+    uint64_t wave_grid = 0;            // heavy stage, wave mode: workgroups (0 = from the last call's heavy count)
+    uint64_t wave_min_rem = 4;         // heavy stage, wave mode: nodes with at most this many events left skip the memo
+    unsigned long long* wave_stats = nullptr;   // diagnostic (wave_stats_ptr): 2 x u64 (max, sum of DFS iterations)
     unsigned long long* memo_stats = nullptr;   // diagnostic (memo_stats_ptr): 8 x u64 per heavy-stage group
     uint64_t memo_stats_groups = 0;             // (memo_stats_groups)
     uint32_t memo_lds = 1;                      // heavy-stage memo tables in LDS: 0 never, 1 short lists, 2 always
     uint64_t giant_grid = 0;           // giant stage workgroups (0 = 2 per CU)
     uint64_t giant_stall_us = 0;       // diagnostic: the giant stage's first frontier chunk starts this late
-    // heavy stage: one wavefront per history (wave_search) unless the last
-    // finished call sent more than wave_max histories there (then one lane
-    // per history, memo_search); heavy_mode 0 / 1 forces wave / lane
-    uint64_t heavy_mode = 1;
+    // heavy stage: one wavefront per history (wave_search, csrc/wave.hip)
+    // unless the last finished call sent more than wave_max histories there
+    // (then one lane per history, memo_search, csrc/memo.hip); heavy_mode
+    // 0 / 1 forces wave / lane mode, 2 (default) picks
+    uint64_t heavy_mode = 2;
     uint64_t wave_max = 16384;
-    bool lane_mode = false;
     uint32_t* probe_host = nullptr;    // pinned: [defer, heavy32, heavy64, giant, timed] of the last finished call
     uint32_t* debug_host = nullptr;    // QSMD_SYNC_STAGES: giant-stage heartbeat (pinned)
     // lane mode's tables: one per lane slot of the memo grid
-    uint64_t memo_grid = 4096;         // heavy stage (lane mode): workgroups at most; one private table each
+    uint64_t memo_grid = 0;            // heavy stage (lane mode): workgroups at most (0 = 12 per CU); one table each
     uint64_t mt_entries = 256;
     char* mt = nullptr;
     size_t mt_bytes = 0;
     uint32_t mt_epoch = 0;
-    bool mt_failed = false;
     // giant stage: exact-count memo (HBM, shared by the giants of a call)
     uint64_t split_xmemo = 1;
     char* xm = nullptr;
@@ -186,6 +184,7 @@ int fill_model0(qsmd_ctx* c, uint32_t model_id, const void* model0, SearchArgs& 
     a.m0_exists = 0;
     a.m0_just = 0;
     a.m0_small = 1;
+    a.m0_wave = 1;
     for (auto& v : a.m0_val) v = 0;
     if (!model0) return QSMD_OK;
     if (model_id == QSMD_MODEL_BANK) {
@@ -204,8 +203,11 @@ int fill_model0(qsmd_ctx* c, uint32_t model_id, const void* model0, SearchArgs& 
         a.m0_just = m->is_just;
         a.m0_val[0] = m->is_just ? m->n : 0;
     }
-    for (int64_t v : a.m0_val)
+    a.m0_wave = 1;
+    for (int64_t v : a.m0_val) {
         if (v < -(1 << 18) || v >= (1 << 18)) a.m0_small = 0;   // compact stages hold 19-bit values
+        if (v <= -(1 << 24) || v >= (1 << 24)) a.m0_wave = 0;   // wave mode's wide list: +-2^24
+    }
     return QSMD_OK;
 }
 
@@ -289,9 +291,6 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->split_budget = value;
     } else if (n == "split_xmemo") {
         c->split_xmemo = value ? 1 : 0;
-    } else if (n == "wave_budget") {
-        if (value < 1 || value > 0xFFFFFFFFull) return fail(c, QSMD_ERR_ARG, "wave_budget in 1..2^32-1");
-        c->wave_budget = value;
     } else if (n == "wave_grid") {
         if (value > 65536) return fail(c, QSMD_ERR_ARG, "wave_grid in 0..65536");
         c->wave_grid = value;
@@ -303,7 +302,7 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->giant_stall_us = value;
     } else if (n == "wave_min_rem") {
         c->wave_min_rem = std::min<uint64_t>(value, 0xFFFFFFFFull);
-    } else if (n == "wave_stats_ptr") {     // diagnostic: device buffer of 8 x u64 per wave_search workgroup
+    } else if (n == "wave_stats_ptr") {     // diagnostic: device buffer of 2 x u64 (zeroed by the caller)
         c->wave_stats = reinterpret_cast<unsigned long long*>(value);
     } else if (n == "memo_stats_ptr") {     // diagnostic: device buffer of 8 x u64 per heavy-stage group (zeroed)
         c->memo_stats = reinterpret_cast<unsigned long long*>(value);
@@ -318,7 +317,7 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "wave_max") {
         c->wave_max = value;
     } else if (n == "memo_grid") {
-        if (value < 1 || value > 65536) return fail(c, QSMD_ERR_ARG, "memo_grid in 1..65536");
+        if (value > 65536) return fail(c, QSMD_ERR_ARG, "memo_grid in 0..65536 (0 = 12 per CU)");
         if (value != c->memo_grid && c->mt) {
             quiesce(c);
             (void)hipFree(c->mt);
@@ -326,7 +325,6 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
             c->mt_bytes = 0;
         }
         c->memo_grid = value;
-        c->mt_failed = false;
     } else if (n == "memo_lane_entries") {
         if (value < 2 || value > 65536 || (value & (value - 1)))
             return fail(c, QSMD_ERR_ARG, "memo_lane_entries: a power of two in 2..65536");
@@ -337,7 +335,6 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
             c->mt_bytes = 0;
         }
         c->mt_entries = value;
-        c->mt_failed = false;
     } else {
         return fail(c, QSMD_ERR_ARG, "unknown parameter");
     }
@@ -387,9 +384,6 @@ static int memo_prepare(qsmd_ctx* c, hipStream_t s, unsigned long long** out) {
     return QSMD_OK;
 }
 
-// Lane mode's tables (3 GB by default), allocated on first use; false when
-// the device cannot hold them (the context then stays in wave mode: the same
-// results, a different speed).
 // A tail stage's grid: one workgroup per 64 histories the last call sent
 // there, between 2 per CU and `cap` (cap before the first call).
 static uint64_t tail_grid(const qsmd_ctx* c, uint64_t cap, uint64_t last) {
@@ -397,18 +391,23 @@ static uint64_t tail_grid(const qsmd_ctx* c, uint64_t cap, uint64_t last) {
     return std::min<uint64_t>(cap, std::max<uint64_t>(2ull * c->n_cu, (last + 63) / 64));
 }
 
-static bool lane_tables(qsmd_ctx* c, hipStream_t s) {
-    const size_t need = (size_t)c->memo_grid * 64 * c->mt_entries * (32 + 64);
-    if (c->mt_failed) return false;
+// Lane mode's HBM memo tables for a heavy-stage grid of `grid` workgroups
+// (one private table per lane slot: grid x 64 x entries x (32 + 64) B),
+// grown on demand and cleared once when (re)allocated -- entries are tagged
+// by call epoch, never cleared per call.  False when the device cannot hold
+// them: the call then runs the heavy stage in wave mode (the same results).
+static bool lane_tables(qsmd_ctx* c, hipStream_t s, uint64_t grid) {
+    const size_t need = (size_t)grid * 64 * c->mt_entries * (32 + 64);
     if (c->mt_bytes >= need) return true;
     bool re = false;
     if (grow(c, &c->mt, &c->mt_bytes, need, &re) != QSMD_OK) {
-        c->mt_failed = true;
-        c->err = "lane-mode memo tables do not fit on the device: wave mode only";
+        (void)hipGetLastError();
         return false;
     }
     if (hipMemsetAsync(c->mt, 0, c->mt_bytes, s) != hipSuccess) {
-        c->mt_failed = true;
+        (void)hipFree(c->mt);
+        c->mt = nullptr;
+        c->mt_bytes = 0;
         return false;
     }
     return true;
@@ -430,18 +429,29 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
 
     // the previous call of this context may run on another stream
     if (c->in_flight && c->last_stream != s) HIP_TRY(c, hipStreamWaitEvent(s, c->done_ev, 0), "hipStreamWaitEvent");
-    // heavy-stage mode from the last finished call's probe
-    if (c->heavy_mode == 2 && c->any_call && hipEventQuery(c->done_ev) == hipSuccess)
-        c->lane_mode = (uint64_t)c->probe_host[1] + c->probe_host[2] > c->wave_max;
-    else if (c->heavy_mode != 2)
-        c->lane_mode = c->heavy_mode == 1;
-    const bool lane = c->lane_mode && lane_tables(c, s);
     // the tail launches' grids from the last finished call's list sizes (a
     // hint: every tail kernel is grid-stride, any grid gives the same
     // results); none before a call has finished
     if (!c->probe_valid && c->any_call && hipEventQuery(c->done_ev) == hipSuccess) c->probe_valid = true;
-    uint32_t hint[4];
-    for (int i = 0; i < 4; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
+    uint32_t hint[6];
+    for (int i = 0; i < 6; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
+    // heavy-stage mode: lane mode (64 searches per wavefront instruction) for
+    // a long heavy list, wave mode (one search per wavefront, its DFS chain
+    // ~10x shorter) for a short one -- by the last finished call's count
+    const uint64_t heavy_hint = c->probe_valid ? (uint64_t)hint[1] + hint[2] : 0ull;
+    bool lane = c->heavy_mode == 1 || (c->heavy_mode == 2 && heavy_hint > c->wave_max);
+    // lane mode's memo tables in LDS (one wavefront per CU) when the last
+    // call's heavy groups fit the CUs, else in HBM (one table per lane slot)
+    const bool wide = hint[2] != 0u;   // G64 groups in the launch only when the last call had some
+    const uint64_t g32 = c->probe_valid ? ((uint64_t)hint[1] + 63u) / 64u : ~0ull;
+    const bool lt = c->memo_lds == 2 || (c->memo_lds == 1 && g32 <= (uint64_t)c->n_cu);
+    // (LDS tables: one workgroup per CU, so no idle workgroups beyond
+    // twice the groups expected -- they would hold CUs the next call's
+    // stage 0 could use)
+    const uint64_t mg = lt && !wide ? std::min<uint64_t>(c->n_cu, 2 * std::min<uint64_t>(g32, c->n_cu) + 8)
+                                    : tail_grid(c, c->memo_grid ? c->memo_grid : 12ull * c->n_cu,
+                                                c->probe_valid ? heavy_hint : ~0ull);
+    if (lane && !(lt && !wide)) lane = lane_tables(c, s, mg);
 
     // ---- workspace: header, lists, giant records, tasks
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
@@ -450,7 +460,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const size_t off_l0 = kWsHeader;                     // stage 0 -> stage 0w
     const size_t off_h32 = off_l0 + lst;                 // heavy lists
     const size_t off_h64 = off_h32 + lst;
-    const size_t off_lg = off_h64 + lst;                 // giants
+    const size_t off_lw = off_h64 + lst;                 // stage 0w's deferred (wide) histories
+    const size_t off_lg = off_lw + lst;                  // giants
     const size_t off_gr = off_lg + lst;
     const size_t off_tk = off_gr + align_up(n_hist * sizeof(GiantRec));
     const size_t off_ts = off_tk + align_up(n_tk * sizeof(qsmd_task));
@@ -471,6 +482,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     uint32_t* l0 = reinterpret_cast<uint32_t*>(c->ws + off_l0);
     uint32_t* h32 = reinterpret_cast<uint32_t*>(c->ws + off_h32);
     uint32_t* h64 = reinterpret_cast<uint32_t*>(c->ws + off_h64);
+    uint32_t* lw = reinterpret_cast<uint32_t*>(c->ws + off_lw);
     uint32_t* lg = reinterpret_cast<uint32_t*>(c->ws + off_lg);
     if (early && !nodes) nodes = reinterpret_cast<uint64_t*>(c->ws + off_nd);
 
@@ -513,8 +525,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     SearchArgs aw = a;
     aw.list = l0;
     aw.list_count = cnt + C_DEFER;
-    aw.defer_list = lg;
-    aw.defer_count = cnt + C_GIANT;
+    aw.defer_list = lw;                      // (wave mode searches most of them; the rest: giants)
+    aw.defer_count = cnt + C_WIDE;
     aw.heavy_list = h64;
     aw.heavy_count = cnt + C_HEAVY64;
     aw.stage0_budget = c->stage0w_budget ? c->stage0w_budget : ~0ull;
@@ -523,11 +535,11 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // ---- heavy stage: histories over the stage budgets
     const uint64_t cap = split ? 64 * c->split_budget : 0;
     if (lane) {
-        if (((++c->mt_epoch) & 0xFFFFFFu) == 0u) {   // 24-bit tags wrapped: clear
+        if (((++c->mt_epoch) & 0xFFFFFFu) == 0u && c->mt) {   // 24-bit tags wrapped: clear
             HIP_TRY(c, hipMemsetAsync(c->mt, 0, c->mt_bytes, s), "memset memo tables");
             ++c->mt_epoch;
         }
-        const uint64_t slots = c->memo_grid * 64 * c->mt_entries;
+        const uint64_t slots = mg * 64 * c->mt_entries;
         MemoArgs mp[2]{};
         for (int w = 0; w < 2; ++w) {
             mp[w].s = a;
@@ -539,18 +551,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].giant_cap = cap;
             mp[w].stats = c->memo_stats;
             mp[w].stats_groups = c->memo_stats ? c->memo_stats_groups : 0;
+            mp[w].fwd_list = lw;                 // stage 0w's deferred histories: on to the giant stage
+            mp[w].fwd_count = cnt + C_WIDE;
         }
-        // G64 groups in this launch only when the last call had some (else they go to the giant stage)
-        const bool wide = hint[2] != 0u;
-        // the memo tables in LDS (one wavefront per CU) when the last call's
-        // heavy groups fit the CUs: the stage is then one search's latency
-        const uint64_t g32 = c->probe_valid ? ((uint64_t)hint[1] + 63u) / 64u : ~0ull;
-        const bool lt = c->memo_lds == 2 || (c->memo_lds == 1 && g32 <= (uint64_t)c->n_cu);
-        // (LDS tables: one workgroup per CU, so no idle workgroups beyond
-        // twice the groups expected -- they would hold CUs the next call's
-        // stage 0 could use)
-        const uint64_t mg = lt && !wide ? std::min<uint64_t>(c->n_cu, 2 * std::min<uint64_t>(g32, c->n_cu) + 8)
-                                        : tail_grid(c, c->memo_grid, (uint64_t)hint[1] + hint[2]);
         HIP_TRY(c, launch_memo(mp[0], mp[1], (uint32_t)mg, wide, lt, s), "memo launch");
         stage_done("lane", s, cnt);
     } else {
@@ -560,17 +563,23 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         wp.count32 = cnt + C_HEAVY32;
         wp.list64 = h64;
         wp.count64 = cnt + C_HEAVY64;
-        wp.next32 = cnt + C_NEXT32;
-        wp.next64 = cnt + C_NEXT64;
-        wp.budget = c->wave_budget;
+        wp.list_wide = lw;
+        wp.count_wide = cnt + C_WIDE;
         wp.explore_cap = cap;
+        wp.explore_cap_wide = split ? 16 * c->split_budget : 0;   // (the giant stage's whole-search cap)
         wp.stats = c->wave_stats;
         wp.memo_min_rem = (uint32_t)c->wave_min_rem;
-        if (max_nodes) {
-            const uint64_t mcap = 16 * max_nodes + 64 * c->wave_budget;
-            wp.explore_cap = wp.explore_cap ? std::min(wp.explore_cap, mcap) : mcap;
-        }
-        const uint64_t g = c->wave_grid ? c->wave_grid : 3ull * c->n_cu;
+        wp.memo_mode = (flags & QSMD_FLAG_MEMO) ? 1u : 0u;
+        // LDS memo table: 8 KB per wavefront (256 entries of <= 64 events),
+        // 64 KB when the last call had wide histories (1024 entries of <= 128)
+        const uint64_t wide_hint = c->probe_valid ? (uint64_t)hint[kProbeWide] : 0ull;
+        wp.buckets = wide_hint ? 256u : 32u;
+        // one workgroup per history the last call sent here (+ 25 %), at
+        // least 64 and at most 16 per CU (grid-stride beyond)
+        const uint64_t nh = heavy_hint + wide_hint;
+        const uint64_t g = c->wave_grid ? c->wave_grid
+                         : std::min<uint64_t>(16ull * c->n_cu,
+                                              c->probe_valid ? std::max<uint64_t>(64, nh + nh / 4) : 4ull * c->n_cu);
         HIP_TRY(c, launch_wave(wp, (uint32_t)g, s), "wave launch");
         stage_done("wave", s, cnt);
     }

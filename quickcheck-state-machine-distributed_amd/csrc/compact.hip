@@ -40,14 +40,14 @@ namespace qsmd {
 
 // Run one lane's search to its end (status), with the early-exit and time
 // limit checks every 1024 iterations.
-template <int MODE, class DFS>
+template <class DFS>
 __device__ __forceinline__ int run_search(DFS& dfs, const SearchArgs& a, const uint32_t* evc,
                                           int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t h,
                                           uint64_t t0) {
     int status;
     uint32_t iter = 0;
     do {                                 // one exit (see LaneDFS::step)
-        status = dfs.template step<C_LANES, MODE>(a, evc, s_bal, lane, limit);
+        status = dfs.template step<C_LANES>(a, evc, s_bal, lane, limit);
         ++iter;
         if ((iter & 1023u) == 0u && status < 0) {
             if (beyond_first_fail(a, h)) {
@@ -80,7 +80,7 @@ __device__ __forceinline__ int stage_fresh(const SearchArgs& a, bool fresh, uint
                         (uint64_t)H.ev_off + n_ev <= a.n_events;
     const bool small = enc_ok && n_ev <= (uint32_t)G::EV && n_pid <= 8u && a.m0_small;
 
-    StagedT<M> s{0, 0, 0, 0, 0, true, true, false};
+    StagedT<M> s{0, 0, 0, 0, 0, true, true};
     // a block: the fresh histories (a prefix of the lanes) with the first
     // one's length, back to back
     const uint64_t F = __ballot(fresh);
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
         const bool search = status == -1;
         const uint32_t n_ev = H.n_ev;
         // the general path (pid masks): finish_lane does not pair (lane.h)
-        if (search) status = run_search<M_GENERAL>(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
+        if (search) status = run_search(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
         note_failure(a, h, status);
         // over the stage budget (not the caller's): searched again by the heavy stage
         const bool heavy = tiered && status == QSMD_STATUS_BUDGET && dfs.nodes >= limit;

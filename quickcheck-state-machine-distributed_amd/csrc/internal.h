@@ -7,13 +7,14 @@
 //                                  a node budget          (csrc/compact.hip)
 //   stage 0w  compact_search<G64>  the histories stage 0 cannot hold, <= 64
 //                                  events                 (csrc/compact.hip)
-//   heavy     memo_search          the histories over the stage-0 / 0w
-//                                  budgets (both lists, one launch), one per
-//                                  lane with an exact-count HBM memo
-//                                  (csrc/memo.hip; heavy_mode 1, default), or
-//                                  wave_search, one wavefront per history
-//                                  with an LDS memo (csrc/wave.hip; heavy_mode
-//                                  0, or 2 = by the last call's count)
+//   heavy     wave_search          the histories over the stage-0 / 0w
+//                                  budgets (both lists, one launch): one
+//                                  wavefront per history, scalar DFS, LDS
+//                                  memo (csrc/wave.hip) -- or, for a long
+//                                  list, memo_search: one lane per history
+//                                  with an exact-count memo (csrc/memo.hip);
+//                                  heavy_mode 2 (default) picks by the last
+//                                  call's count
 //   giants    giant_search         everything else: the split stage (one
 //                                  history over many lanes), the ordered
 //                                  combine, the batch totals (csrc/split.hip)
@@ -57,6 +58,7 @@ enum Cnt : uint32_t {
     C_XNEXT,            // early-exit fixup queue head
     C_XDONE,            // fixup chunks finished
     C_EXIT,             // giant-stage blocks finished
+    C_WIDE,             // stage 0w -> wave mode's wide list (or, in lane mode, on to the giant stage)
     C_N = 32
 };
 
@@ -92,6 +94,7 @@ struct SearchArgs {
     uint32_t m0_exists;
     uint32_t m0_just;
     uint32_t m0_small;            // every model0 value within 19-bit signed (compact stages)
+    uint32_t m0_wave;             // every model0 value within +-2^24 (wave mode's wide list)
     int64_t m0_val[QSMD_BANK_MAX_ACCOUNTS];
     // outputs
     uint8_t* status;
@@ -107,6 +110,10 @@ struct SearchArgs {
     uint32_t* giant_list;
     uint32_t* giant_count;
 };
+
+// qsmd_ctx::probe_host slots: [C_DEFER, C_HEAVY32, C_HEAVY64, C_GIANT,
+// C_TIMED] of the last finished call, then its wide-list count
+constexpr int kProbeWide = 5;
 
 // internal status: the search was handed to a later stage (not a result)
 constexpr int QSMD_STATUS_HANDED_OFF = 0x40;
@@ -203,20 +210,24 @@ __host__ __device__ inline int combine_tasks(uint32_t term_status, uint64_t term
 
 // ------------------------------------------------------------ heavy stage
 // wave_search (csrc/wave.hip): one wavefront per history of list32 (<= 32
-// events) then list64 (<= 64 events); histories it cannot finish within
-// explore_cap iterations go to the giant stage.
+// events), list64 (<= 64 events) and list_wide (<= 128 events, <= 8 pids;
+// the rest of it goes on to the giant stage), the DFS in wave-uniform
+// registers with an LDS state memo per wavefront; histories it cannot finish
+// within explore_cap iterations go to the giant stage.
 struct WaveArgs {
     SearchArgs s;
     const uint32_t* list32;
     const uint32_t* count32;
     const uint32_t* list64;
     const uint32_t* count64;
-    uint32_t* next32;             // queue heads (zeroed per call)
-    uint32_t* next64;
-    uint64_t budget;              // nodes a task searches before it may split
-    uint64_t explore_cap;         // iterations per history before the giant stage (0 = none)
+    const uint32_t* list_wide;    // stage 0w's deferred histories (> 64 events or wide values)
+    const uint32_t* count_wide;
+    uint64_t explore_cap;         // iterations per heavy history before the giant stage (0 = none)
+    uint64_t explore_cap_wide;    // the same for the wide list
     uint32_t memo_min_rem;        // nodes with at most this many events left are not memoised
-    unsigned long long* stats;    // diagnostic: 8 x u64 per workgroup (null in production)
+    uint32_t memo_mode;           // QSMD_FLAG_MEMO: a memo hit counts nothing (explored nodes)
+    uint32_t buckets;             // LDS memo table: buckets of 64 words (a power of two)
+    unsigned long long* stats;    // diagnostic: [max, sum] of DFS iterations per history (null in production)
 };
 hipError_t launch_wave(const WaveArgs& p, uint32_t grid, hipStream_t s);
 
@@ -231,6 +242,8 @@ struct MemoArgs {
     uint64_t giant_cap;           // > 0: a search past this many iterations goes to s.giant_list
     unsigned long long* stats;    // diagnostic (memo_stats_ptr): 8 x u64 per group of the launch, or null
     uint64_t stats_groups;        // groups the stats buffer holds
+    const uint32_t* fwd_list;     // appended to s.giant_list as they are (stage 0w's wide list)
+    const uint32_t* fwd_count;
 };
 // lds_tables: the G32 memo tables in LDS (ignored with `wide`)
 hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool lds_tables,

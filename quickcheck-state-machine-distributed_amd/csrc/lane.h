@@ -1,7 +1,6 @@
 // lane.h -- the per-lane search machinery shared by the compact-domain
 // kernels (csrc/compact.hip: stages 0 and 0w; csrc/memo.hip: the heavy
-// stage in lane mode; csrc/wave.hip: the heavy stage in wave mode): the
-// compressed event format, the staging paths, and LaneDFS, the reference
+// stage in lane mode): the compressed event format, the staging paths, and LaneDFS, the reference
 // DFS (src/Linearisability.hs:25-69 over the Lemma L1 event bitset) as a
 // per-lane state machine for histories of at most 32 (G32) or 64 (G64)
 // events and 8 pids.
@@ -23,20 +22,16 @@ constexpr int C_CHUNK = 16;
 constexpr int32_t V19_MIN = -(1 << 18), V19_MAX = (1 << 18) - 1;   // model0 values (api.hip m0_small)
 
 // compressed event (one u32 per event, LDS [event][lane]):
-//   invocation  pid 3 | 0 | code 3 | a 3 | b 3 | r 5 | val 14 (signed)
+//   invocation  pid 3 | 0 | code 3 | a 3 | b 3 | 0 (5 bits) | val 14 (signed)
 //   response    pid 3 | 1 | code 3 | val 25 (signed)
-// r: in a paired history (every pid alternates invocation / response), the
-// index of the response paired with the invocation (0 = none: pending);
-// filled only by wave mode's finish_shared (finish_lane leaves it 0: the
-// compact stages run the general path).
 // Staging writes a marker instead of an event it cannot hold: an invocation
 // with code 7 (not an encodable event: ENCODE_ERROR) or code 6 (a value
 // outside the ranges above: the history goes to the next stage).
 constexpr int32_t IVAL_BITS = 14, RVAL_BITS = 25;
 constexpr uint32_t MARK_BAD = 0x70u, MARK_WIDE = 0x60u;
 // Geometry of a compact stage: <= 32 events (u32 event masks, 16 levels,
-// r 5 bits, invocation values 14 bits) or <= 64 events (u64, 32 levels,
-// r 6 bits, invocation values 13 bits).  Response words are the same.
+// invocation values 14 bits, stack entries j 5 bits) or <= 64 events (u64,
+// 32 levels, 13 bits, j 6 bits).  Response words are the same.
 struct G32 {
     using M = uint32_t;
     static constexpr int EV = 32, RB = 5, IVB = 14, LEVELS = 16;
@@ -49,8 +44,6 @@ struct G64 {
 __device__ __forceinline__ uint32_t c_code(uint32_t w) { return (w >> 4) & 7u; }
 __device__ __forceinline__ uint32_t c_a(uint32_t w) { return (w >> 7) & 7u; }
 __device__ __forceinline__ uint32_t c_b(uint32_t w) { return (w >> 10) & 7u; }
-template <class G = G32>
-__device__ __forceinline__ uint32_t c_r(uint32_t w) { return (w >> 13) & ((1u << G::RB) - 1u); }
 template <class G = G32>
 __device__ __forceinline__ int32_t c_ival(uint32_t w) { return (int32_t)w >> (32 - G::IVB); }
 __device__ __forceinline__ int32_t c_rval(uint32_t w) { return (int32_t)w >> (32 - RVAL_BITS); }
@@ -213,7 +206,7 @@ struct StackN {
 template <class M>
 struct StagedT {
     M INV, RESP, P0, P1, P2;
-    bool ok, fits, paired;
+    bool ok, fits;
 };
 using Staged = StagedT<uint32_t>;
 
@@ -370,43 +363,6 @@ __device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane,
     s.P2 = P2;
     s.ok = ((BAD & ALL) | GEP) == (M)0;
     s.fits = (WIDE & ALL) == (M)0;
-    s.paired = false;
-}
-
-// finish_lane for a history shared by the wavefront (csrc/wave.hip): every
-// lane derives the same masks from s_hist[e]; only `writer` ORs the pairs in.
-template <class G = G32>
-__device__ __forceinline__ void finish_shared(uint32_t* s_hist, bool writer, uint32_t n_ev, uint32_t n_pid,
-                                              StagedT<typename G::M>& s) {
-    using M = typename G::M;
-    // s_hist[e] is read at step e; the writer only ORs into earlier words
-    uint32_t open = 0u, ps_lo = 0u, ps_hi = 0u, unpaired = 0u, bad = 0u, wide = 0u;
-#pragma unroll
-    for (uint32_t e = 0; e < (uint32_t)G::EV; ++e) {
-        if (e >= n_ev) break;
-        const uint32_t w = s_hist[e];
-        const M bit = (M)1 << e;
-        const uint32_t p = w & 7u, resp = (w >> 3) & 1u, mk = w & 0x78u;
-        bad |= ((mk == MARK_BAD) | (p >= n_pid)) ? 1u : 0u;
-        wide |= mk == MARK_WIDE ? 1u : 0u;
-        s.RESP |= resp ? bit : (M)0;
-        s.INV |= resp ? (M)0 : bit;
-        s.P0 |= (w & 1u) ? bit : (M)0;
-        s.P1 |= (w & 2u) ? bit : (M)0;
-        s.P2 |= (w & 4u) ? bit : (M)0;
-        const uint32_t ob = (open >> p) & 1u, sh = (p & 3u) * 8u;
-        const bool hi = p >= 4u;
-        const uint32_t j = ((hi ? ps_hi : ps_lo) >> sh) & (uint32_t)(G::EV - 1);
-        unpaired |= resp ? (ob ^ 1u) : ob;
-        open ^= (resp ? ob : (ob ^ 1u)) << p;
-        const uint32_t ins = (ps_lo & ~(0xFFu << sh)) | (e << sh), insh = (ps_hi & ~(0xFFu << sh)) | (e << sh);
-        ps_lo = (!resp && !hi) ? ins : ps_lo;
-        ps_hi = (!resp && hi) ? insh : ps_hi;
-        if (writer && resp && ob) s_hist[j] |= e << 13;
-    }
-    s.ok = bad == 0u;
-    s.fits = wide == 0u;
-    s.paired = unpaired == 0u;
 }
 
 // --------------------------------------------------------------- the DFS
@@ -414,12 +370,9 @@ __device__ __forceinline__ void finish_shared(uint32_t* s_hist, bool writer, uin
 // Per-lane search state (registers) over the history in LDS column `lane`.
 // step() runs one iteration: an optional backtrack followed by one
 // candidate try; it returns -1 to continue or the final QSMD_STATUS_*
-// (QSMD_STATUS_BUDGET = `limit` nodes reached before a decision).
-// MODE: M_GENERAL (any pid pattern: the response and the removed invocation
-// come from the bit-sliced pid masks), M_PAIRED (every history of the
-// wavefront is paired: the response index is read from the invocation word)
-// or M_LANE (per-lane `paired` flag).
-enum { M_GENERAL = 0, M_PAIRED = 1, M_LANE = 2 };
+// (QSMD_STATUS_BUDGET = `limit` nodes reached before a decision).  Any pid
+// pattern: the response and the removed invocation come from the
+// bit-sliced pid masks.
 
 template <uint32_t MODEL, class G = G32>
 struct LaneDFS {
@@ -431,7 +384,6 @@ struct LaneDFS {
     M rem, cand;
     uint32_t depth, ex, neg, RS, found;
     uint32_t base;          // depth of the search root (0; the task depth in split_search)
-    bool paired;
     uint32_t last_j;        // candidate of the most recent try (the one a BUDGET return did not count)
     uint64_t nodes;
     StackN<G::LEVELS / 4> stk;
@@ -449,7 +401,6 @@ struct LaneDFS {
         rem = ALL;
         cand = cands(rem, INV, RESP);
         depth = 0; found = 0; nodes = 0; RS = 0; base = 0;
-        paired = s.paired;
 #pragma unroll
         for (int q = 0; q < G::LEVELS / 4; ++q) stk.w[q] = 0u;
         ex = a.m0_exists; neg = 0;
@@ -468,19 +419,15 @@ struct LaneDFS {
     // a history shared by the wavefront: STRIDE = 1)
     // Undo the last level: restore the parent node's state exactly
     // (remaining events, model); returns the candidate the level went through.
-    template <int STRIDE, int MODE>
+    template <int STRIDE>
     __device__ __forceinline__ uint32_t undo(const uint32_t* evc, int32_t (*s_bal)[C_LANES], int lane) {
         --depth;
         const uint32_t st = stk.top();
         stk.pop();
         const uint32_t j = st & JM;
-        const uint32_t cj = (BANK || MODE != M_GENERAL) ? evc[j * STRIDE] : 0u;
-        if (is_paired<MODE>()) {
-            rem |= ((M)1 << j) | ((M)1 << c_r<G>(cj));
-        } else {
-            const M gone = ~rem & same_pid(j);
-            rem |= ((M)1 << m_hibit(gone & INV)) | ((M)1 << m_hibit(gone & RESP));
-        }
+        const uint32_t cj = BANK ? evc[j * STRIDE] : 0u;
+        const M gone = ~rem & same_pid(j);
+        rem |= ((M)1 << m_hibit(gone & INV)) | ((M)1 << m_hibit(gone & RESP));
         if constexpr (BANK) {
             const uint32_t code = c_code(cj), ia = c_a(cj), ib = c_b(cj);
             const int32_t m = c_ival<G>(cj);
@@ -508,12 +455,7 @@ struct LaneDFS {
         return j;
     }
 
-    template <int MODE>
-    __device__ __forceinline__ bool is_paired() const {
-        return MODE == M_PAIRED || (MODE == M_LANE && paired);
-    }
-
-    template <int STRIDE, int MODE = M_GENERAL>
+    template <int STRIDE>
     __device__ __forceinline__ int step(const SearchArgs& a, const uint32_t* evc,
                                         int32_t (*s_bal)[C_LANES], int lane, uint64_t limit) {
         // one exit at the end (no early returns: the state stays in place
@@ -526,34 +468,26 @@ struct LaneDFS {
                            : ((!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE);
         if (empty & !term) {
             // ---- backtrack: restore the parent level exactly
-            const uint32_t j = undo<STRIDE, MODE>(evc, s_bal, lane);
+            const uint32_t j = undo<STRIDE>(evc, s_bal, lane);
             cand = cands(rem, INV, RESP) & mask_above(j, (M)0);
             found = 1u;
         }
-        if (cand) status = try_next<STRIDE, MODE>(a, evc, s_bal, lane, limit);
+        if (cand) status = try_next<STRIDE>(a, evc, s_bal, lane, limit);
         return status;
     }
 
     // ---- try the next candidate: straight-line, predicated
-    template <int STRIDE, int MODE>
+    template <int STRIDE>
     __device__ __forceinline__ int try_next(const SearchArgs& a, const uint32_t* evc,
                                             int32_t (*s_bal)[C_LANES], int lane, uint64_t limit) {
         const uint32_t j = m_ctz(cand);
         cand &= cand - (M)1;
         last_j = j;
         const uint32_t cj = evc[j * STRIDE];
-        uint32_t r;
-        M pmj = 0;
-        bool has;                              // findResponse => [] : no child
-        if (is_paired<MODE>()) {
-            r = c_r<G>(cj);
-            has = r != 0u;
-        } else {
-            pmj = same_pid(j);
-            const M rr = rem & pmj & RESP;
-            has = rr != (M)0;
-            r = m_ctz(rr | ((M)1 << JM));
-        }
+        const M pmj = same_pid(j);
+        const M rr = rem & pmj & RESP;
+        const bool has = rr != (M)0;           // findResponse => [] : no child
+        const uint32_t r = m_ctz(rr | ((M)1 << JM));
         const uint32_t cr = evc[r * STRIDE];
         const uint32_t code = c_code(cj), rc = c_code(cr);
         const int32_t m = c_ival<G>(cj), rv = c_rval(cr);
@@ -618,7 +552,7 @@ struct LaneDFS {
         stk.push_if(ok, stw);
         depth += ok ? 1u : 0u;
         const M fi = rem & pmj & INV;
-        const M rem2 = rem & ~((is_paired<MODE>() ? ((M)1 << j) : (fi & ((M)0 - fi))) | ((M)1 << r));
+        const M rem2 = rem & ~((fi & ((M)0 - fi)) | ((M)1 << r));
         rem = ok ? rem2 : rem;
         cand = ok ? cands(rem2, INV, RESP) : cand;
         found = ok ? 0u : found;

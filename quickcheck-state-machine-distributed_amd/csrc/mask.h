@@ -38,6 +38,7 @@ struct M128 {
     uint64_t lo, hi;   // trivial aggregate: usable in __shared__ arrays
     __device__ __forceinline__ M128 operator&(const M128& o) const { return {lo & o.lo, hi & o.hi}; }
     __device__ __forceinline__ M128 operator|(const M128& o) const { return {lo | o.lo, hi | o.hi}; }
+    __device__ __forceinline__ M128 operator^(const M128& o) const { return {lo ^ o.lo, hi ^ o.hi}; }
     __device__ __forceinline__ M128 operator~() const { return {~lo, ~hi}; }
     __device__ __forceinline__ M128& operator&=(const M128& o) { lo &= o.lo; hi &= o.hi; return *this; }
     __device__ __forceinline__ M128& operator|=(const M128& o) { lo |= o.lo; hi |= o.hi; return *this; }

@@ -148,7 +148,7 @@ __device__ __forceinline__ void memo_insert_lds(uint32_t* col, const MemoKey<MOD
 // One DFS iteration with the memo (LaneDFS::step plus the two hooks).
 // entry: the lane's column of node counts at entry, per level; tab: the
 // lane's HBM table, or (LT) its LDS column.
-template <uint32_t MODEL, class G, int MODE, bool LT>
+template <uint32_t MODEL, class G, bool LT>
 __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* evc,
                                          int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* tab,
                                          uint32_t h, uint32_t epoch, uint32_t mask, uint32_t* entry, bool& skip) {
@@ -169,13 +169,13 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
             }
         }
         skip = false;
-        const uint32_t j = d.template undo<C_LANES, MODE>(evc, s_bal, lane);
+        const uint32_t j = d.template undo<C_LANES>(evc, s_bal, lane);
         d.cand = cands(d.rem, d.INV, d.RESP) & mask_above(j, (M)0);
         d.found = 1u;
     }
     if (d.cand) {
         const uint32_t dep0 = d.depth;
-        status = d.template try_next<C_LANES, MODE>(a, evc, s_bal, lane, limit);
+        status = d.template try_next<C_LANES>(a, evc, s_bal, lane, limit);
         if (d.depth > dep0 && status < 0) {       // entered a new node (and the search goes on)
             entry[dep0 * C_LANES] = (uint32_t)d.nodes;
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
@@ -243,7 +243,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
     qsmd_hdr H;
     if (active) H = a.hdr[h];
     else H = qsmd_hdr{0, 0, 0, 0, 0, 0};
-    StagedT<M> s{0, 0, 0, 0, 0, true, true, false};
+    StagedT<M> s{0, 0, 0, 0, 0, true, true};
     if (active) {
         stage_lane<MODEL, G>(a, H, L.ev, lane);
         finish_lane<G>(L.ev, lane, H.n_ev, H.n_pid, s);
@@ -276,7 +276,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
         uint32_t iter = 0;
         do {
             const bool was = skip;
-            status = memo_step<MODEL, G, M_GENERAL, LT>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch, mask,
+            status = memo_step<MODEL, G, LT>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch, mask,
                                                  &L.entry[0][lane], skip);
             if constexpr (ST) hits += (!was && skip) ? 1u : 0u;
             ++iter;
@@ -335,6 +335,12 @@ __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32,
     if constexpr (LT) {
         lcol = lds + sizeof(MemoLds<MODEL, G32>) / 4u + lane;
         for (uint32_t e = 0; e < kLdsEntries; ++e) lcol[e * 8u * C_LANES] = kNoHistory;
+    }
+    // stage 0w's wide list goes on to the giant stage (wave mode searches it)
+    const uint32_t nf = *p32.fwd_count;
+    for (uint32_t b = blockIdx.x * C_LANES; b < nf; b += gridDim.x * C_LANES) {
+        const bool in = b + (uint32_t)lane < nf;
+        wave_append(in, in ? p32.fwd_list[b + lane] : 0u, p32.s.giant_list, p32.s.giant_count, lane);
     }
     for (uint64_t grp = blockIdx.x; grp < n32 + n64; grp += gridDim.x) {
         unsigned long long* q = p32.stats && grp < p32.stats_groups ? p32.stats + grp * 8u : nullptr;

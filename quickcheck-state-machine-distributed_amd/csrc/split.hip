@@ -843,6 +843,7 @@ __device__ void finish_call(const SplitArgs& p, int lane) {
         reinterpret_cast<unsigned long long*>(p.totals)[lane] = t;
     }
     if (p.probe_host && lane <= (int)C_TIMED) p.probe_host[lane] = p.cnt[lane];
+    if (p.probe_host && lane == kProbeWide) p.probe_host[kProbeWide] = p.cnt[C_WIDE];
     // restore: buckets (and the early-exit ones), then the counters
     for (uint32_t i = (uint32_t)lane; i < kBuckets * kBucketWords; i += 64u) {
         bk[i] = 0ull;

@@ -1,657 +1,523 @@
-// wave.hip -- the heavy stage: one wavefront searches one history with all
-// 64 lanes and a state memo shared by the lanes in LDS (BASELINE north star
-// (a)-(c)).
+// wave.hip -- the heavy stage in wave mode: one wavefront per history, the
+// DFS in wave-uniform (scalar) registers.
 //
-// Stages 0 / 0w search one history per lane with a node budget; the few
-// histories over it (a wavefront runs as long as its slowest lane, so a long
-// search would hold 63 idle lanes and the launch with them) come here.  A
-// wavefront takes one heavy history at a time, stages it once into LDS
-// (shared by its lanes) and searches the reference DFS tree
-// (src/Linearisability.hs:52-69) with every lane:
+// The heavy histories are the few whose search exceeds the compact stages'
+// node budget (config 2: ~1200 of 1M, 40..320 reference nodes each).  In
+// lane mode (csrc/memo.hip) a lane runs one of them, and every DFS step is
+// a chain of dependent LDS round trips (the candidate's event, its response,
+// the balances, the memo probe) that a lone wavefront cannot hide: ~2900
+// cycles per step, so the list's longest search sets the stage's time.
+// Here the whole wavefront owns one history and nothing on the DFS chain
+// touches memory:
+//   * event e of the history sits in lane e (e - 64: a second register) of
+//     two VGPRs, its lo word and its value, read at a wave-uniform index with
+//     v_readlane (an SGPR result);
+//   * Bank balances sit in lanes 0..7 of a VGPR (v_readlane / v_writelane at
+//     the account index), the DFS stack and the per-level node counts in lane
+//     d of two more VGPRs; event masks, the remaining-event set, the model's
+//     small parts and the node count are scalars;
+//   * so a candidate try (src/Linearisability.hs:25-69 at one node:
+//     takeInvocations, findResponse, filter1, postcondition, transition) is
+//     straight scalar code, ~10x shorter than the lane-mode step's memory
+//     chain.
+// The state memo (north star (c)) is exact-count, as in lane mode: a state
+// S = (remaining events, model) is recorded with the nodes its subtree
+// counted when the search leaves it (it failed: the search goes on), and a
+// later entry into S adds that count and backtracks (memo.hip explains why
+// verdict, count and witness stay the reference's).  With QSMD_FLAG_MEMO
+// (explored-node counts) a hit adds nothing and every state is recorded.
+// The table is the wavefront's own, in LDS: buckets of 64 words, one word
+// per lane, holding 8 entries of 8 words (<= 64 events) or 4 of 16 (<= 128),
+// so a probe is ONE ds_read_b32 across the wavefront and a ballot of the 64
+// word compares finds a matching entry.  Entries carry a per-history epoch:
+// nothing is cleared between histories.
 //
-//   task    a region of the tree: the candidates `cand` of the node N at
-//           depth `depth`, with N's exact search state (remaining events,
-//           model, path).  The root task is the whole tree.
-//   split   a lane whose task has counted `budget` more nodes while other
-//           lanes are idle and the pool is empty hands the rest of its task
-//           to the pool: one range task per level between its base and its
-//           current node (the untried candidates of that node), each with
-//           the node's state, restored level by level with the DFS's own
-//           exact undo.  Idle lanes take pending tasks by ballot + prefix
-//           count; the deepest ranges (smallest keys) first.
-//   key     a task's place in the reference's DFS order: digit i =
-//           2*(j+1) for a path step through candidate event j, 2*c+1 at the
-//           task's level for "candidates c, c+1, ... of this node" (keys
-//           compare lexicographically, a prefix first).
-//   fold    the reference stops at the first deciding node (a success, or
-//           Map.! raising).  Its node count = nodes of every task whose key
-//           is below the decider's + the decider's own; when nothing decides,
-//           the sum of all.  Finished tasks are recorded (key, nodes) in LDS;
-//           a record below every running and pending task's key can never be
-//           after a future decider and is folded into a running sum.
-//   cancel  a lane whose task key is above the best decider so far stops at
-//           once; pending tasks above it are dropped.
-//   memo    the subtree below a node depends only on its state S =
-//           (remaining events, model) (SURVEY.md §8a Lemma L1), so its
-//           outcome and node count are a function of S.  A subtree that a
-//           lane searched to its end inside its own task (no split below it)
-//           without deciding has failed; the lane records (S, count) in the
-//           wavefront's LDS table, and any lane entering a node whose S is
-//           recorded adds the count and treats the subtree as failed.  Keys
-//           are the full state (no hash-only match), so counts, verdicts and
-//           witnesses stay the reference's exactly; only the work shrinks.
-//
-// All scheduling is wave-synchronous (ballots, prefix counts, LDS); the only
-// global atomic is the one that hands out the next heavy history.
+// Three lists, one launch: the heavy lists of stages 0 and 0w (<= 32 and
+// <= 64 events) and the histories stage 0w deferred (beyond 64 events, or
+// values beyond the compact encoding): those with <= 128 events, <= 8 pids
+// and values within 2^24 (no i32 overflow in any balance) run here with
+// 128-bit masks, the rest go to the giant stage, as does every search past
+// its iteration cap (the split stage searches it again from the root).
+// Lane mode keeps the long heavy lists (config 3: ~285k heavy histories,
+// where 64 searches per wavefront instruction win); the host picks by the
+// last call's heavy count (api.hip, heavy_mode 2).
 #include <hip/hip_runtime.h>
 
 #include "internal.h"
 #include "lane.h"
+#include "mask.h"
 
 namespace qsmd {
 
 namespace {
 
-constexpr int kPool = 64;                  // pending range tasks per wavefront
-constexpr int kRec = 256;                  // task records per history
-constexpr uint32_t kMemoEntries = 512;     // LDS memo entries per wavefront (power of two)
-constexpr uint32_t kMemoW = 8;             // words per entry (SoA: word w of entry e at w * E + e)
-constexpr uint32_t kTagValid = 0x80000000u;
-constexpr uint32_t kTagClaim = 0x40000000u;
+constexpr uint32_t kEpochMax = 0xFFFFFFu;    // 24-bit entry tags (word 2 = ex | epoch << 8)
+constexpr int32_t kWideValue = 1 << 24;      // wide-list values (and model0) within +-2^24: no i32 overflow
 
-// task key: digit i of DB bits, DPW digits per u64 word, compared
-// lexicographically (G32: 16 digits of 7 bits in 2 words; G64: 32 digits of
-// 8 bits in 4 words -- a path digit 2(j+1) reaches 2*EV)
-template <class G>
-struct CKey {
-    static constexpr int NK = G::EV == 32 ? 2 : 4;
-    static constexpr uint32_t DB = G::EV == 32 ? 7u : 8u;
-    static constexpr uint32_t DPW = 64u / DB;
-    uint64_t w[NK];
-    __device__ __forceinline__ void clear(uint64_t v) {
-#pragma unroll
-        for (int q = 0; q < NK; ++q) w[q] = v;
-    }
-    __device__ __forceinline__ void put(uint32_t i, uint64_t d) {
-        const uint32_t k = i / DPW, sh = 64u - DB * (i % DPW + 1u);
-#pragma unroll
-        for (int q = 0; q < NK; ++q)
-            if ((uint32_t)q == k) w[q] |= d << sh;
-    }
-    __device__ __forceinline__ bool less(const CKey& b) const {
-#pragma unroll
-        for (int q = 0; q < NK; ++q)
-            if (w[q] != b.w[q]) return w[q] < b.w[q];
-        return false;
-    }
-    __device__ __forceinline__ bool operator==(const CKey& b) const {
-        bool e = true;
-#pragma unroll
-        for (int q = 0; q < NK; ++q) e = e && w[q] == b.w[q];
-        return e;
-    }
-};
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int32_t rli(int32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+// (a lane write as a compare + select on the lane id: hipcc emits v_writelane)
+__device__ __forceinline__ uint32_t wl(uint32_t v, uint32_t x, uint32_t l) { return threadIdx.x == l ? x : v; }
+__device__ __forceinline__ int32_t wli(int32_t v, int32_t x, uint32_t l) { return threadIdx.x == l ? x : v; }
 
-// wave-wide minimum of a key (every lane gets it)
-template <class K>
-__device__ __forceinline__ void wave_min_key(K& k) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        K o;
-#pragma unroll
-        for (int q = 0; q < K::NK; ++q) o.w[q] = __shfl_xor(k.w[q], off, 64);
-        if (o.less(k)) k = o;
-    }
+// ---- scalar event-mask helpers: u64 (<= 64 events) and M128 (<= 128)
+__device__ __forceinline__ bool mnz(uint64_t m) { return m != 0ull; }
+__device__ __forceinline__ bool mnz(const M128& m) { return (m.lo | m.hi) != 0ull; }
+__device__ __forceinline__ uint32_t mctz(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
+__device__ __forceinline__ uint32_t mctz(const M128& m) {
+    return m.lo ? (uint32_t)__builtin_ctzll(m.lo) : 64u + (uint32_t)__builtin_ctzll(m.hi);
+}
+__device__ __forceinline__ uint32_t mhibit(uint64_t m) { return 63u - (uint32_t)__builtin_clzll(m); }
+__device__ __forceinline__ uint32_t mhibit(const M128& m) {
+    return m.hi ? 127u - (uint32_t)__builtin_clzll(m.hi) : 63u - (uint32_t)__builtin_clzll(m.lo);
+}
+__device__ __forceinline__ uint32_t mpop(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
+__device__ __forceinline__ uint32_t mpop(const M128& m) {
+    return (uint32_t)(__builtin_popcountll(m.lo) + __builtin_popcountll(m.hi));
+}
+__device__ __forceinline__ uint32_t mbitof(uint64_t m, uint32_t j) { return (uint32_t)(m >> j) & 1u; }
+__device__ __forceinline__ uint32_t mbitof(const M128& m, uint32_t j) {
+    return (uint32_t)((j < 64u ? m.lo : m.hi) >> (j & 63u)) & 1u;
+}
+template <typename M> __device__ __forceinline__ M mbit(uint32_t j);
+template <> __device__ __forceinline__ uint64_t mbit<uint64_t>(uint32_t j) { return 1ull << j; }
+template <> __device__ __forceinline__ M128 mbit<M128>(uint32_t j) {
+    return mk128(j < 64u ? 1ull << (j & 63u) : 0ull, j < 64u ? 0ull : 1ull << (j & 63u));
+}
+template <typename M> __device__ __forceinline__ M msplat(uint32_t b);
+template <> __device__ __forceinline__ uint64_t msplat<uint64_t>(uint32_t b) { return 0ull - (uint64_t)b; }
+template <> __device__ __forceinline__ M128 msplat<M128>(uint32_t b) {
+    return mk128(0ull - (uint64_t)b, 0ull - (uint64_t)b);
+}
+__device__ __forceinline__ uint64_t mlowest(uint64_t m) { return m & (0ull - m); }
+__device__ __forceinline__ M128 mlowest(const M128& m) { return MaskOps<M128>::lowest(m); }
+// the bits above j
+__device__ __forceinline__ uint64_t mabove(uint32_t j, uint64_t) { return ~1ull << j; }
+__device__ __forceinline__ M128 mabove(uint32_t j, const M128&) { return ~MaskOps<M128>::below((int)j + 1); }
+// takeInvocations (src/Linearisability.hs:25-28): remaining invocations
+// below the lowest remaining response
+__device__ __forceinline__ uint64_t mcands(uint64_t rem, uint64_t INV, uint64_t RESP) {
+    const uint64_t rr = rem & RESP;
+    return rem & INV & ((rr & (0ull - rr)) - 1ull);
+}
+__device__ __forceinline__ M128 mcands(const M128& rem, const M128& INV, const M128& RESP) {
+    const M128 rr = rem & RESP;
+    return rem & INV & MaskOps<M128>::below(mnz(rr) ? (int)mctz(rr) : 128);
 }
 
-// exclusive prefix sum over the wavefront
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
-    uint32_t x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
-    return x - v;
-}
+template <typename M> struct Geo;
+template <> struct Geo<uint64_t> { static constexpr uint32_t NW = 1, EW = 8; };     // events / 64, entry words
+template <> struct Geo<M128> { static constexpr uint32_t NW = 2, EW = 16; };
 
-template <class G>
-struct Pool {              // pending range tasks (LDS)
-    using M = typename G::M;
-    using K = CKey<G>;
-    M cand[kPool];
-    uint32_t meta[kPool];  // depth | found << 8
-    M rem[kPool];
-    uint32_t model[kPool]; // Bank: ex | neg << 8; Ticket: RS
-    uint32_t stk[G::LEVELS / 4][kPool];
-    uint64_t key[K::NK][kPool];
-    int32_t bal[QSMD_BANK_MAX_ACCOUNTS][kPool];
-    __device__ __forceinline__ K get_key(uint32_t e) const {
-        K k;
-#pragma unroll
-        for (int q = 0; q < K::NK; ++q) k.w[q] = key[q][e];
-        return k;
+// The reference DFS of one history, wave-uniform (every member is a scalar;
+// the per-event / per-account / per-level arrays are lanes of VGPRs).
+template <uint32_t MODEL, typename M>
+struct WaveDFS {
+    static constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
+    static constexpr uint32_t NW = Geo<M>::NW;
+    M INV, RESP, P0, P1, P2, ALL;
+    M rem, cand;
+    uint64_t nodes;
+    uint64_t RS;            // Ticket: levels whose operation was a Reset
+    uint32_t depth, ex, neg, found;
+    // lanes: lo / val = event e (lane e % 64 of word e / 64), bal = account q
+    // (lane q), stk = the undo record of level d (lane d: j | ex_a << 7 |
+    // ex_b << 8), ent = the node count at entry of level d (lane d)
+    uint32_t lo[NW];
+    int32_t val[NW];
+    int32_t bal;
+    uint32_t stk, ent;
+
+    __device__ __forceinline__ uint32_t ev_lo(uint32_t e) const {
+        if constexpr (NW == 1) {
+            return rl(lo[0], e);
+        } else {
+            const uint32_t x0 = rl(lo[0], e & 63u), x1 = rl(lo[1], e & 63u);
+            return e < 64u ? x0 : x1;
+        }
     }
-    __device__ __forceinline__ void set_key(uint32_t e, const K& k) {
-#pragma unroll
-        for (int q = 0; q < K::NK; ++q) key[q][e] = k.w[q];
+    __device__ __forceinline__ int32_t ev_val(uint32_t e) const {
+        if constexpr (NW == 1) {
+            return rli(val[0], e);
+        } else {
+            const int32_t x0 = rli(val[0], e & 63u), x1 = rli(val[1], e & 63u);
+            return e < 64u ? x0 : x1;
+        }
+    }
+    __device__ __forceinline__ M same_pid(uint32_t j) const {
+        const M m0 = msplat<M>(mbitof(P0, j)), m1 = msplat<M>(mbitof(P1, j)), m2 = msplat<M>(mbitof(P2, j));
+        return ~((P0 ^ m0) | (P1 ^ m1) | (P2 ^ m2)) & ALL;
+    }
+
+    // Undo the last level exactly (remaining events, model); returns its candidate.
+    __device__ __forceinline__ uint32_t undo() {
+        --depth;
+        const uint32_t st = rl(stk, depth);
+        const uint32_t j = st & 127u;
+        const M gone = ~rem & same_pid(j);
+        rem |= mbit<M>(mhibit(gone & INV)) | mbit<M>(mhibit(gone & RESP));
+        if constexpr (BANK) {
+            const uint32_t lj = ev_lo(j);
+            const int32_t m = ev_val(j);
+            const uint32_t code = (lj >> 8) & 0xFFu, ia = (lj >> 16) & 7u, ib = (lj >> 24) & 7u;
+            const uint32_t pa = (st >> 7) & 1u, pb = (st >> 8) & 1u;
+            const bool tr = code == QSMD_BANK_TRANSFER;
+            const int32_t ba = rli(bal, ia), bb = rli(bal, ib);
+            const int32_t rb = (pb || ia == ib) ? bb - m : 0;      // Transfer's deposit on b undone
+            const int32_t cur_a = (tr && ia == ib) ? rb : ba;
+            const int32_t ra = pa ? cur_a - bank_sign(code) * m : 0;
+            bal = wli(bal, tr ? rb : bb, ib);                      // a no-op unless Transfer
+            bal = wli(bal, ra, ia);                                // last (ia == ib)
+            ex = (ex & ~((1u << ia) | ((tr ? 1u : 0u) << ib))) | (pa << ia) | ((tr ? pb : 0u) << ib);
+            neg = 0u;   // the parent held the invariant (a step descends only then)
+        } else {
+            RS &= ~(1ull << depth);
+        }
+        return j;
+    }
+
+    // Ticket model at the current depth: Just (#TT since the last Reset), or
+    // model0 advanced by succ <$> once per level
+    __device__ __forceinline__ void ticket_model(const SearchArgs& a, uint32_t& just, int32_t& n) const {
+        just = RS ? 1u : a.m0_just;
+        n = RS ? (int32_t)(depth - 1u - (63u - (uint32_t)__builtin_clzll(RS | 1ull)))
+               : (int32_t)a.m0_val[0] + (a.m0_just ? (int32_t)depth : 0);
+    }
+
+    // Try the next candidate of the current node (LaneDFS::try_next, scalar):
+    // -1 to go on, or QSMD_STATUS_BUDGET / QSMD_STATUS_MODEL_ERROR.
+    __device__ __forceinline__ int try_next(const SearchArgs& a, uint64_t limit) {
+        const uint32_t j = mctz(cand);
+        cand &= ~mbit<M>(j);
+        const M pm = same_pid(j);
+        const M rr = rem & pm & RESP;
+        const bool has = mnz(rr);                                  // findResponse => [] : no child
+        const uint32_t r = has ? mctz(rr) : j;
+        const uint32_t lj = ev_lo(j), lr = ev_lo(r);
+        const int32_t m = ev_val(j), rv = ev_val(r);
+        const uint32_t code = (lj >> 8) & 0xFFu, rc = (lr >> 8) & 0xFFu;
+        const bool over = has && nodes >= limit;
+        bool ok, err = false;
+        uint32_t stw = j;
+        if constexpr (BANK) {
+            const uint32_t ia = (lj >> 16) & 7u, ib = (lj >> 24) & 7u;
+            const int32_t bal_a = rli(bal, ia), bal_b = rli(bal, ib);
+            const uint32_t ex_a = (ex >> ia) & 1u, ex_b = (ex >> ib) & 1u;
+            // post (test/Bank.hs:118-131): invariant && the expected response
+            const bool tr = code == QSMD_BANK_TRANSFER, chk = code == QSMD_BANK_CHECK_BALANCE;
+            const bool same = ia == ib;
+            const uint32_t sel = (code == QSMD_BANK_OPEN_ACCOUNT || bal_a >= m) ? ex_a : 0u;
+            const uint32_t exp = (kBankExp2 >> (code * 6u + sel * 3u)) & 7u;
+            const bool inv_ok = neg == 0u;
+            err = has && inv_ok && chk && rc == QSMD_BANK_BALANCE && !ex_a;   // Map.! raises
+            ok = has && !over && inv_ok && !err && rc == exp && (!chk || rv == bal_a);
+            stw = j | (ex_a << 7) | (ex_b << 8);
+            if (ok) {
+                // next' (test/Bank.hs:92-101): insertWith on a, then Transfer's deposit on b
+                const int32_t sa = bank_sign(code);
+                const int32_t na = (ex_a ? bal_a : 0) + (ex_a ? sa : (sa & 1)) * m;
+                const int32_t bo = same ? na : bal_b;
+                const int32_t fb = tr ? (((ex_b != 0u) || same) ? bo : 0) + m : bo;
+                bal = wli(bal, na, ia);
+                bal = wli(bal, fb, ib);
+                const int32_t va = same ? fb : na;
+                ex |= ((chk ? 0u : 1u) << ia) | ((tr ? 1u : 0u) << ib);
+                neg = (va | fb) < 0 ? 1u : 0u;
+            }
+        } else {
+            // TicketDispenser (test/TicketDispenser.hs:81-102)
+            uint32_t just;
+            int32_t tn;
+            ticket_model(a, just, tn);
+            const bool tt = code == QSMD_TICKET_TAKE_TICKET;
+            ok = has && !over && (tt ? (rc == QSMD_TICKET_NUMBER && just != 0u && rv == tn + 1)
+                                     : rc == QSMD_TICKET_OK);
+            if (ok && !tt) RS |= 1ull << depth;
+        }
+        const bool counted = has && !over;
+        nodes += counted ? 1u : 0u;
+        found |= counted ? 1u : 0u;
+        if (ok) {
+            stk = wl(stk, stw, depth);
+            ++depth;
+            const M fi = rem & pm & INV;                           // filter1: the pid's first invocation
+            rem &= ~(mlowest(fi) | mbit<M>(r));
+            cand = mcands(rem, INV, RESP);
+            found = 0u;
+        }
+        return over ? QSMD_STATUS_BUDGET : (err ? QSMD_STATUS_MODEL_ERROR : -1);
     }
 };
 
-template <class G>
-struct Recs {              // finished tasks of the current history (LDS)
-    using K = CKey<G>;
-    uint64_t key[K::NK][kRec];
-    uint64_t nodes[kRec];
-    __device__ __forceinline__ K get_key(uint32_t e) const {
-        K k;
-#pragma unroll
-        for (int q = 0; q < K::NK; ++q) k.w[q] = key[q][e];
-        return k;
-    }
-    __device__ __forceinline__ void set_key(uint32_t e, const K& k) {
-#pragma unroll
-        for (int q = 0; q < K::NK; ++q) key[q][e] = k.w[q];
-    }
-};
-
-template <class G>
-struct WaveLds {
-    uint32_t hist[G::EV];                              // the history, compressed (lane.h)
-    int32_t bal[QSMD_BANK_MAX_ACCOUNTS][C_LANES];      // Bank balances [account][lane]
-    uint32_t entry[G::LEVELS][C_LANES];                // node count (low 32 bits) on entering a level
-    Pool<G> pool;
-    Recs<G> rec;
-    uint8_t path[G::LEVELS];                           // the best witness path
-};
-
-__device__ __forceinline__ uint32_t wmix(uint32_t h) {
-    h ^= h >> 16;
-    h *= 0x7FEB352Du;
-    h ^= h >> 15;
-    h *= 0x846CA68Bu;
-    h ^= h >> 16;
-    return h;
-}
-
-// The memo key of a lane's current node: tag (valid | model flags), the
-// remaining events, the model (Bank: balances of the existing accounts as
-// i16, absent = 0; Ticket: n).  ok = false: the state is outside the key
-// encoding (a balance beyond i16) and is not memoised.
+// The memo key of the current state in lane layout: lane l holds word l % EW
+// of an entry: 0, 1 rem bits 0-63, 2 ex | epoch << 8, 3 count, 4..7 model
+// (Bank balances as i16 pairs, Ticket just | n << 1), and for 128-bit masks
+// 8, 9 rem bits 64-127 (10..15 zero).  `ok` false when the state does not
+// fit (a balance beyond i16): not recorded, not looked up.
 struct WKey {
-    uint32_t tag, rem_lo, rem_hi, m[4], slot;
+    uint32_t vec;       // this lane's word
+    uint32_t bucket;
     bool ok;
 };
 
-template <uint32_t MODEL, class G>
-__device__ __forceinline__ WKey wave_key(const LaneDFS<MODEL, G>& d, const SearchArgs& a,
-                                         int32_t (*s_bal)[C_LANES], int lane) {
-    WKey k;
-    k.ok = true;
-    k.rem_lo = (uint32_t)d.rem;
-    k.rem_hi = G::EV == 64 ? (uint32_t)((uint64_t)d.rem >> 32) : 0u;
+template <uint32_t MODEL, typename M>
+__device__ __forceinline__ WKey wave_key(const WaveDFS<MODEL, M>& d, const SearchArgs& a, uint32_t epoch,
+                                         uint32_t bucket_mask, int lane) {
+    uint32_t m[4];
+    bool ok = true;
     if constexpr (MODEL == QSMD_MODEL_BANK) {
-        const uint32_t ex = d.ex;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int32_t b0 = ((ex >> (2 * q)) & 1u) ? s_bal[2 * q][lane] : 0;
-            const int32_t b1 = ((ex >> (2 * q + 1)) & 1u) ? s_bal[2 * q + 1][lane] : 0;
-            k.ok = k.ok && b0 == (int32_t)(int16_t)b0 && b1 == (int32_t)(int16_t)b1;
-            k.m[q] = ((uint32_t)b0 & 0xFFFFu) | ((uint32_t)b1 << 16);
+            const int32_t b0 = rli(d.bal, 2 * q), b1 = rli(d.bal, 2 * q + 1);
+            ok = ok && b0 == (int32_t)(int16_t)b0 && b1 == (int32_t)(int16_t)b1;
+            m[q] = ((uint32_t)b0 & 0xFFFFu) | ((uint32_t)b1 << 16);
         }
-        k.tag = kTagValid | (ex & 0xFFu);
     } else {
-        // the model after levels 0 .. depth-1 (LaneDFS::try_next's formula)
-        const uint32_t just = d.RS ? 1u : a.m0_just;
-        const int32_t n = d.RS ? (int32_t)(d.depth - 1u - (31u - __builtin_clz(d.RS | 1u)))
-                               : (int32_t)a.m0_val[0] + (a.m0_just ? (int32_t)d.depth : 0);
-        k.m[0] = just ? (uint32_t)n : 0u;
-        k.m[1] = k.m[2] = k.m[3] = 0u;
-        k.tag = kTagValid | just;
+        uint32_t just;
+        int32_t n;
+        d.ticket_model(a, just, n);
+        m[0] = just | (just ? (uint32_t)n << 1 : 0u);
+        m[1] = m[2] = m[3] = 0u;
     }
-    uint32_t h = wmix(k.rem_lo ^ 0x9E3779B9u);
-    h = wmix(h ^ k.rem_hi ^ k.tag);
+    uint32_t r0, r1, r2 = 0u, r3 = 0u;
+    if constexpr (Geo<M>::NW == 1) {
+        r0 = (uint32_t)d.rem;
+        r1 = (uint32_t)(d.rem >> 32);
+    } else {
+        r0 = (uint32_t)d.rem.lo;
+        r1 = (uint32_t)(d.rem.lo >> 32);
+        r2 = (uint32_t)d.rem.hi;
+        r3 = (uint32_t)(d.rem.hi >> 32);
+    }
+    const uint32_t w2 = (MODEL == QSMD_MODEL_BANK ? d.ex : 0u) | (epoch << 8);
+    const uint32_t v = (m[0] ^ __builtin_amdgcn_alignbit(m[1], m[1], 8)) ^
+                       (__builtin_amdgcn_alignbit(m[2], m[2], 16) ^ __builtin_amdgcn_alignbit(m[3], m[3], 24));
+    uint32_t hsh = (r0 * 0x9E3779B1u) ^ ((r1 ^ w2) * 0x85EBCA77u) ^ (v * 0xC2B2AE3Du) ^
+                   ((r2 ^ __builtin_amdgcn_alignbit(r3, r3, 16)) * 0x27D4EB2Fu);
+    hsh ^= (hsh >> 16) ^ (hsh >> 24);
+    const uint32_t w = (uint32_t)lane & (Geo<M>::EW - 1u);
+    uint32_t x = w == 0u ? r0 : 0u;
+    x = w == 1u ? r1 : x;
+    x = w == 2u ? w2 : x;
+    x = w == 4u ? m[0] : x;
+    x = w == 5u ? m[1] : x;
+    x = w == 6u ? m[2] : x;
+    x = w == 7u ? m[3] : x;
+    if constexpr (Geo<M>::EW == 16) {
+        x = w == 8u ? r2 : x;
+        x = w == 9u ? r3 : x;
+    }
+    return WKey{x, hsh & bucket_mask, ok};
+}
+
+// One probe: the bucket's entries (one word per lane); the count of the
+// matching entry, if any.  Group g of EW bits of the ballot = entry g.
+template <uint32_t EW>
+__device__ __forceinline__ bool wave_lookup(const uint32_t* tab, const WKey& k, int lane, uint32_t& count) {
+    constexpr uint64_t ONES = EW == 8 ? 0x0101010101010101ull : 0x0001000100010001ull;
+    constexpr uint64_t HIGH = ONES << (EW - 1u);
+    const uint32_t w = tab[k.bucket * 64u + (uint32_t)lane];
+    const uint64_t eq = __ballot(w == k.vec) | (ONES << 3);   // word 3 (the count) is not compared
+    const uint64_t z = ~eq;                                    // a zero group: every word matched
+    const uint64_t t = (z - ONES) & ~z & HIGH;
+    if (t == 0ull) return false;
+    const uint32_t e = (uint32_t)__builtin_ctzll(t) / EW;      // the lowest flagged group is exact
+    count = rl(w, e * EW + 3u);
+    return true;
+}
+
+template <uint32_t EW>
+__device__ __forceinline__ void wave_insert(uint32_t* tab, const WKey& k, uint32_t count, uint32_t victim,
+                                            int lane) {
+    if (((uint32_t)lane / EW) == (victim % (64u / EW)))
+        tab[k.bucket * 64u + (uint32_t)lane] = ((uint32_t)lane % EW) == 3u ? count : k.vec;
+}
+
+// One history h (its header H) searched by the whole wavefront (wide: from
+// stage 0w's deferred list).
+template <uint32_t MODEL, typename M>
+__device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, const qsmd_hdr& H, bool wide,
+                                             uint32_t* tab, uint32_t epoch, uint32_t& victim, int lane, uint64_t t0,
+                                             Counters& cnt) {
+    constexpr uint32_t NW = Geo<M>::NW, EW = Geo<M>::EW;
+    const SearchArgs& a = p.s;
+    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
+    const uint32_t n_ev = H.n_ev;
+    WaveDFS<MODEL, M> d;
+    // staging: lane l loads events l (and l + 64): coalesced 8-B loads
+    bool bad = false, big = false;
+    uint64_t bl[NW][6];            // ballots: RESP, P0, P1, P2, ALL, (unused)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) h = wmix(h ^ k.m[q]);
-    k.slot = h & (kMemoEntries - 1u);
-    return k;
-}
-
-__device__ __forceinline__ bool wave_lookup(const uint32_t* tab, const WKey& k, uint32_t& count) {
-    const uint32_t s = k.slot;
-    constexpr uint32_t E = kMemoEntries;
-    const bool hit = tab[s] == k.tag && tab[E + s] == k.rem_lo && tab[2 * E + s] == k.rem_hi &&
-                     tab[4 * E + s] == k.m[0] && tab[5 * E + s] == k.m[1] && tab[6 * E + s] == k.m[2] &&
-                     tab[7 * E + s] == k.m[3];
-    count = tab[3 * E + s];
-    return hit;
-}
-
-// Lanes inserting into one slot in the same instruction: the first CAS of
-// the tag word claims the slot, the others leave it (a cache entry lost, no
-// result changes); the winner writes the key and count, the tag last.
-__device__ __forceinline__ void wave_insert(uint32_t* tab, const WKey& k, uint32_t count, int lane) {
-    const uint32_t s = k.slot;
-    constexpr uint32_t E = kMemoEntries;
-    const uint32_t cur = __hip_atomic_load(&tab[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    const uint32_t mine = kTagClaim | (uint32_t)lane;
-    const uint32_t old = atomicCAS(&tab[s], cur, mine);
-    if (old == cur) {
-        tab[E + s] = k.rem_lo;
-        tab[2 * E + s] = k.rem_hi;
-        tab[3 * E + s] = count;
-        tab[4 * E + s] = k.m[0];
-        tab[5 * E + s] = k.m[1];
-        tab[6 * E + s] = k.m[2];
-        tab[7 * E + s] = k.m[3];
-        __hip_atomic_store(&tab[s], k.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    for (uint32_t w = 0; w < NW; ++w) {
+        const uint32_t e = (uint32_t)lane + 64u * w;
+        const bool in = e < n_ev;
+        const uint2 x = in ? a.events[H.ev_off + e] : make_uint2(0u, 0u);
+        d.lo[w] = x.x;
+        d.val[w] = (int32_t)x.y;
+        const uint32_t pid = x.x & 0x7Fu;
+        bad = bad || (in && (!valid_bits<MODEL>(x.x) || pid >= H.n_pid));
+        big = big || (in && (x.x & 0x80u) == 0u && ((int32_t)x.y >= kWideValue || (int32_t)x.y <= -kWideValue));
+        bl[w][0] = __ballot(in && (x.x & 0x80u));
+        bl[w][1] = __ballot(in && (pid & 1u));
+        bl[w][2] = __ballot(in && (pid & 2u));
+        bl[w][3] = __ballot(in && (pid & 4u));
+        bl[w][4] = __ballot(in);
     }
-}
+    if constexpr (NW == 1) {
+        d.RESP = bl[0][0]; d.P0 = bl[0][1]; d.P1 = bl[0][2]; d.P2 = bl[0][3]; d.ALL = bl[0][4];
+    } else {
+        d.RESP = mk128(bl[0][0], bl[1][0]);
+        d.P0 = mk128(bl[0][1], bl[1][1]);
+        d.P1 = mk128(bl[0][2], bl[1][2]);
+        d.P2 = mk128(bl[0][3], bl[1][3]);
+        d.ALL = mk128(bl[0][4], bl[1][4]);
+    }
+    d.INV = d.ALL & ~d.RESP;
+    d.rem = d.ALL;
+    d.cand = mcands(d.rem, d.INV, d.RESP);
+    d.depth = 0u;
+    d.found = 0u;
+    d.nodes = 0ull;
+    d.RS = 0ull;
+    d.stk = 0u;
+    d.ent = 0u;
+    d.ex = a.m0_exists;
+    const bool e_q = (uint32_t)lane < QSMD_BANK_MAX_ACCOUNTS && ((a.m0_exists >> (uint32_t)lane) & 1u);
+    d.bal = e_q ? (int32_t)a.m0_val[lane & 7] : 0;
+    d.neg = __ballot(e_q && d.bal < 0) != 0ull ? 1u : 0u;
 
-// One DFS iteration of a lane (LaneDFS::step) with the memo hooks: on
-// leaving a node entered inside the current task, record its subtree; on
-// entering a node, reuse a recorded subtree.
-template <uint32_t MODEL, class G, int MODE>
-__device__ __forceinline__ int wave_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* hist,
-                                         int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* entry,
-                                         bool& skip, uint32_t* tab, uint32_t min_rem) {
-    using M = typename G::M;
-    const bool empty = d.cand == (M)0;
-    const bool term = empty & ((d.found == 0u) | (d.depth == d.base));
-    int status = !term ? -1
-                       : ((!d.found && d.depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE);
-    if (empty & !term) {
-        // leaving the node at depth d.depth (> base): its subtree was searched
-        // to the end by this lane and failed (counts exact below 2^32)
-        if (!skip && d.nodes <= 0xFFFFFFFFull && (uint32_t)__builtin_popcountll((uint64_t)d.rem) > min_rem) {
-            const WKey k = wave_key<MODEL, G>(d, a, s_bal, lane);
-            if (k.ok) wave_insert(tab, k, (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES], lane);
+    int status = -1;
+    if (__ballot(bad) != 0ull) {
+        status = QSMD_STATUS_ENCODE_ERROR;
+    } else if (wide && __ballot(big) != 0ull) {
+        status = QSMD_STATUS_HANDED_OFF;         // values the i32 model may overflow on: the giant stage
+    } else if (n_ev == 0u) {
+        status = QSMD_STATUS_LINEARISABLE;
+    } else if (beyond_first_fail(a, h)) {
+        status = QSMD_STATUS_SKIPPED;
+    }
+    bool skip = false;
+    uint64_t iter = 0;
+    const uint32_t min_rem = p.memo_min_rem;
+    const bool counts = !p.memo_mode;            // exact counts (else QSMD_FLAG_MEMO: explored nodes)
+    const uint64_t cap = wide ? p.explore_cap_wide : p.explore_cap;
+    while (status < 0) {
+        const bool empty = !mnz(d.cand);
+        if (empty && (d.found == 0u || d.depth == 0u)) {
+            // no children: a leaf => True (any' []), the root => False (any [])
+            status = (d.found == 0u && d.depth > 0u) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE;
+            break;
         }
-        skip = false;
-        const uint32_t j = d.template undo<1, MODE>(hist, s_bal, lane);
-        d.cand = cands(d.rem, d.INV, d.RESP) & mask_above(j, (M)0);
-        d.found = 1u;
-    }
-    if (d.cand) {
-        const uint32_t dep0 = d.depth;
-        status = d.template try_next<1, MODE>(a, hist, s_bal, lane, limit);
-        if (d.depth > dep0 && status < 0 &&
-            (uint32_t)__builtin_popcountll((uint64_t)d.rem) > min_rem) {   // entered a new node (the search goes on)
-            entry[dep0 * C_LANES] = (uint32_t)d.nodes;
-            const WKey k = wave_key<MODEL, G>(d, a, s_bal, lane);
-            uint32_t c = 0;
-            if (k.ok && wave_lookup(tab, k, c)) {
-                d.nodes += c;                     // the subtree's nodes, counted; it failed
-                d.cand = (M)0;
-                d.found = 1u;
-                skip = true;
+        if (empty) {
+            // leaving the node at depth d.depth: its subtree was searched to the end and failed
+            if (!skip && (!counts || d.nodes <= 0xFFFFFFFFull) && mpop(d.rem) > min_rem) {
+                const WKey k = wave_key<MODEL, M>(d, a, epoch, p.buckets - 1u, lane);
+                if (k.ok) wave_insert<EW>(tab, k, counts ? (uint32_t)d.nodes - rl(d.ent, d.depth - 1u) : 0u,
+                                          victim++, lane);
+            }
+            skip = false;
+            const uint32_t j = d.undo();
+            d.cand = mcands(d.rem, d.INV, d.RESP) & mabove(j, d.rem);
+            d.found = 1u;
+        }
+        if (mnz(d.cand)) {
+            const uint32_t dep0 = d.depth;
+            status = d.try_next(a, limit);
+            if (d.depth > dep0 && status < 0) {                // entered a new node (the search goes on)
+                d.ent = wl(d.ent, (uint32_t)d.nodes, dep0);
+                if (mpop(d.rem) > min_rem) {
+                    const WKey k = wave_key<MODEL, M>(d, a, epoch, p.buckets - 1u, lane);
+                    uint32_t c = 0;
+                    if (k.ok && wave_lookup<EW>(tab, k, lane, c)) {
+                        if (counts && d.nodes + c > limit) {   // the budget falls inside that subtree
+                            d.nodes = limit;
+                            status = QSMD_STATUS_BUDGET;
+                        } else {
+                            d.nodes += counts ? c : 0u;        // its nodes, counted; it failed
+                            d.cand = M{};
+                            d.found = 1u;
+                            skip = true;
+                        }
+                    }
+                }
+            }
+        }
+        ++iter;
+        if (status < 0) {
+            if (cap && iter >= cap) {
+                status = QSMD_STATUS_HANDED_OFF;
+            } else if ((iter & 1023u) == 0u) {
+                if (beyond_first_fail(a, h)) {
+                    status = QSMD_STATUS_SKIPPED;
+                } else if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
+                    if (lane == 0) atomicOr(a.timed_out, 1u);
+                    status = QSMD_STATUS_BUDGET;
+                }
             }
         }
     }
-    return status;
+    if (p.stats && lane == 0) {
+        atomicMax(p.stats + 0, (unsigned long long)iter);
+        atomicAdd(p.stats + 1, (unsigned long long)iter);
+    }
+    if (status == QSMD_STATUS_HANDED_OFF) {          // the giant stage searches it (exact, from the root)
+        if (lane == 0) a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
+        return;
+    }
+    if (lane == 0) {
+        note_failure(a, h, status);
+        a.status[h] = (uint8_t)status;
+        if (a.nodes) a.nodes[h] = d.nodes;
+        cnt.add(status, d.nodes);
+    }
+    if (a.witness && status == QSMD_STATUS_LINEARISABLE) {
+        uint8_t* w = a.witness + H.ev_off;
+        if ((uint32_t)lane < d.depth) w[lane] = (uint8_t)(d.stk & 127u);
+        else if ((uint32_t)lane == d.depth && d.depth < n_ev) w[lane] = QSMD_WITNESS_END;
+    }
+}
+
+__device__ __forceinline__ void clear_table(uint32_t* tab, uint32_t buckets, int lane) {
+    for (uint32_t b = 0; b < buckets; ++b) tab[b * 64u + (uint32_t)lane] = 0xFFFFFFFFu;   // word 2 never matches
 }
 
 }  // namespace
 
-template <uint32_t MODEL, int MODE, class G>
-__device__ void wave_history(const WaveArgs& p, uint32_t h, const qsmd_hdr& H, const StagedT<typename G::M>& s,
-                             WaveLds<G>& L, uint32_t* tab, int lane, uint64_t t0, Counters& cnt) {
-    constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
-    using M = typename G::M;
-    using K = CKey<G>;
-    constexpr uint32_t JM = (uint32_t)G::EV - 1u;
-    const SearchArgs& a = p.s;
-    Pool<G>& pool = L.pool;
-    Recs<G>& rec = L.rec;
-    LaneDFS<MODEL, G> dfs;
-    dfs.init(s, a, L.bal, lane);                 // every lane: masks, model0 (the root's state)
-    bool busy = lane == 0;                       // lane 0 starts the root task
-    bool skip = false;
-    K key, best;
-    key.clear(0ull);
-    best.clear(~0ull);
-    uint64_t limit = p.budget;
-    uint32_t pool_n = 0, rec_n = 0;              // wave-uniform
-    uint64_t prefix_sum = 0, explored = 0;
-    uint32_t best_status = QSMD_STATUS_NONLINEARISABLE, best_depth = 0, work = 0;
-    bool incomplete = false, timed = false, skipped = false, overflow = false;
-    uint32_t tick = 0, n_splits = 0;
-    const uint64_t c0 = p.stats ? __builtin_amdgcn_s_memtime() : 0;
-
-    // record the finished task of every lane with `done` (wave-synchronous)
-    auto record = [&](bool done, uint64_t nodes) {
-        const uint64_t m = __ballot(done);
-        if (!m) return;
-        const uint32_t k = lane_prefix(m);
-        if (done) {
-            const uint32_t i = rec_n + k;        // room is kept for every running lane
-            rec.set_key(i, key);
-            rec.nodes[i] = nodes;
-        }
-        rec_n += (uint32_t)__builtin_popcountll(m);
-    };
-
-    // fold the records below min(every running / pending key, best decider)
-    // into prefix_sum, drop the ones above the best decider
-    auto compact = [&]() {
-        K mk;
-        if (busy) mk = key;
-        else mk.clear(~0ull);
-        for (uint32_t i = lane; i < pool_n; i += 64) {
-            const K pk = pool.get_key(i);
-            if (pk.less(mk)) mk = pk;
-        }
-        wave_min_key(mk);
-        if (best.less(mk)) mk = best;
-        uint32_t kept = 0;
-        uint64_t folded = 0;
-        for (uint32_t c0 = 0; c0 < rec_n; c0 += 64) {
-            const uint32_t i = c0 + lane;
-            const bool in = i < rec_n;
-            K rk;
-            rk.clear(0ull);
-            uint64_t rn = 0;
-            if (in) {
-                rk = rec.get_key(i);
-                rn = rec.nodes[i];
-            }
-            const bool below = in && rk.less(mk);
-            const bool after = in && best.less(rk);
-            const bool keep = in && !below && !after;
-            overflow |= __builtin_add_overflow(folded, below ? rn : 0ull, &folded);
-            const uint64_t km = __ballot(keep);
-            if (keep) {                          // in place, in order (kept <= i)
-                const uint32_t d = kept + lane_prefix(km);
-                rec.set_key(d, rk);
-                rec.nodes[d] = rn;
-            }
-            kept += (uint32_t)__builtin_popcountll(km);
-        }
-        // (a sum beyond 2^64 - 1 anywhere: the giant stage reports it)
-        const uint64_t f = wave_sum64(folded);
-        overflow |= __ballot(f < folded) != 0ull;
-        overflow |= __builtin_add_overflow(prefix_sum, f, &prefix_sum);
-        overflow = __ballot(overflow) != 0ull;
-        rec_n = kept;
-    };
-
-    for (;;) {
-        ++tick;
-        // ---- idle lanes take pending tasks (LIFO: the deepest ranges of the
-        // last split, i.e. the smallest keys, first)
-        {
-            const uint64_t idle = __ballot(!busy);
-            const uint32_t take = min((uint32_t)__builtin_popcountll(idle), pool_n);
-            if (take) {
-                const uint32_t k = lane_prefix(idle);
-                if (!busy && k < take) {
-                    const uint32_t e = pool_n - 1u - k;
-                    key = pool.get_key(e);
-                    if (!best.less(key)) {       // else: after the decider, dropped
-                        const uint32_t meta = pool.meta[e];
-                        dfs.cand = pool.cand[e];
-                        dfs.depth = meta & 0xFFu;
-                        dfs.base = dfs.depth;
-                        dfs.found = (meta >> 8) & 1u;
-                        dfs.rem = pool.rem[e];
-                        const uint32_t mdl = pool.model[e];
-                        if constexpr (BANK) {
-                            dfs.ex = mdl & 0xFFu;
-                            dfs.neg = (mdl >> 8) & 0xFFu;
-#pragma unroll
-                            for (int q = 0; q < QSMD_BANK_MAX_ACCOUNTS; ++q) L.bal[q][lane] = pool.bal[q][e];
-                        } else {
-                            dfs.RS = mdl;
-                        }
-#pragma unroll
-                        for (int q = 0; q < G::LEVELS / 4; ++q) dfs.stk.w[q] = pool.stk[q][e];
-                        dfs.nodes = 0;
-                        limit = p.budget;
-                        skip = false;
-                        busy = true;
-                    }
-                }
-                pool_n -= take;
-            }
-        }
-        const uint64_t busy_m = __ballot(busy);
-        if (!busy_m) break;                      // nothing runs, nothing waits: done
-        // ---- one DFS iteration on every busy lane
-        int st = -1;
-        if (busy) {
-            st = wave_step<MODEL, G, MODE>(dfs, a, L.hist, L.bal, lane, limit, &L.entry[0][lane], skip, tab,
-                                           p.memo_min_rem);
-            ++work;
-            if (st < 0 && best.less(key)) st = QSMD_STATUS_SKIPPED;   // cancelled
-        }
-        if ((tick & 63u) == 0u) {
-            if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
-                timed = true;
-                if (lane == 0) atomicOr(a.timed_out, 1u);
-            }
-            if (beyond_first_fail(a, h)) skipped = true;
-            if (p.explore_cap && explored + wave_sum64(work) > p.explore_cap) incomplete = true;
-            if (timed || skipped || incomplete) break;
-        }
-        // ---- task budget reached: split when lanes are idle and nothing waits
-        const bool at_budget = busy && st == QSMD_STATUS_BUDGET && dfs.nodes >= limit;
-        const bool hungry = __ballot(!busy) != 0ull && pool_n == 0u;
-        uint32_t k_ranges = 0;
-        if (at_budget && hungry) {
-            // ranges: the current node's untried candidates (+ the one the
-            // budget did not count), then each ancestor level's later ones
-            M r = dfs.rem;
-            k_ranges = (dfs.cand | ((M)1 << dfs.last_j)) ? 1u : 0u;
-            for (uint32_t l = dfs.depth; l-- > dfs.base;) {
-                const uint32_t j = dfs.stk.get(l, dfs.depth) & JM;
-                if (MODE == M_PAIRED) {
-                    r |= ((M)1 << j) | ((M)1 << c_r<G>(L.hist[j]));
-                } else {
-                    const M gone = ~r & dfs.same_pid(j);
-                    r |= ((M)1 << m_hibit(gone & dfs.INV)) | ((M)1 << m_hibit(gone & dfs.RESP));
-                }
-                k_ranges += (cands(r, dfs.INV, dfs.RESP) & mask_above(j, (M)0)) ? 1u : 0u;
-            }
-        }
-        uint32_t off = 0, tot = 0;
-        if (__ballot(k_ranges != 0u)) {
-            off = wave_excl_scan(k_ranges, lane);
-            tot = __shfl(off + k_ranges, 63, 64);
-        }
-        // room: pool entries, and a record for every task that may still
-        // finish (running, pending, new)
-        const uint32_t running = (uint32_t)__builtin_popcountll(busy_m);
-        if (tot && rec_n + running + pool_n + tot > (uint32_t)kRec) compact();
-        const bool room = rec_n + running + pool_n + tot <= (uint32_t)kRec && pool_n + tot <= (uint32_t)kPool;
-        bool split_done = false;
-        if (at_budget && hungry && room && k_ranges) {
-            // emit: entry index pool_n + off + (k_ranges - 1 - i), i = 0 at
-            // the deepest level (popped first)
-            uint32_t i = 0;
-            auto emit = [&](M c) {
-                const uint32_t e = pool_n + off + (k_ranges - 1u - i);
-                ++i;
-                K k;
-                k.clear(0ull);
-                for (uint32_t d = 0; d < dfs.depth; ++d) k.put(d, 2ull * ((dfs.stk.get(d, dfs.depth) & JM) + 1u));
-                k.put(dfs.depth, 2ull * m_ctz(c) + 1ull);
-                pool.set_key(e, k);
-                pool.cand[e] = c;
-                pool.meta[e] = dfs.depth | ((uint32_t)dfs.found << 8);
-                pool.rem[e] = dfs.rem;
-                if constexpr (BANK) {
-                    pool.model[e] = (dfs.ex & 0xFFu) | ((dfs.neg & 0xFFu) << 8);
-#pragma unroll
-                    for (int q = 0; q < QSMD_BANK_MAX_ACCOUNTS; ++q) pool.bal[q][e] = L.bal[q][lane];
-                } else {
-                    pool.model[e] = dfs.RS;
-                }
-#pragma unroll
-                for (int q = 0; q < G::LEVELS / 4; ++q) pool.stk[q][e] = dfs.stk.w[q];
-            };
-            const M top = dfs.cand | ((M)1 << dfs.last_j);
-            if (top) emit(top);
-            while (dfs.depth > dfs.base) {
-                const uint32_t j = dfs.template undo<1, MODE>(L.hist, L.bal, lane);
-                dfs.found = 1u;
-                const M c = cands(dfs.rem, dfs.INV, dfs.RESP) & mask_above(j, (M)0);
-                if (c) emit(c);
-            }
-            split_done = true;
-        } else if (at_budget) {
-            dfs.cand |= (M)1 << dfs.last_j;      // search on (a memo hit may have jumped past the limit)
-            limit = dfs.nodes + p.budget;
-        }
-        if (tot && room) {
-            pool_n += tot;                       // the ranges of the lanes that split
-            ++n_splits;
-        }
-        // ---- finished tasks: records, the best decider
-        // (a BUDGET return is always a task budget: the caller's max_nodes is
-        // applied by the fold)
-        const bool fin = busy && (split_done || (st >= 0 && st != QSMD_STATUS_BUDGET && st != QSMD_STATUS_SKIPPED));
-        const bool decided = busy && (st == QSMD_STATUS_LINEARISABLE || st == QSMD_STATUS_MODEL_ERROR);
-        if (p.explore_cap && __ballot(fin)) {
-            explored += wave_sum64(fin ? work : 0u);
-            work = fin ? 0u : work;
-        }
-        record(fin, dfs.nodes);
-        if (__ballot(decided)) {
-            K dk;
-            if (decided) dk = key;
-            else dk.clear(~0ull);
-            wave_min_key(dk);
-            if (dk.less(best)) {
-                best = dk;
-                const bool me = decided && key == dk;
-                const uint64_t mm = __ballot(me);
-                const int w = __builtin_ctzll(mm);
-                best_status = (uint32_t)__shfl(st, w, 64);
-                best_depth = (uint32_t)__shfl(dfs.depth, w, 64);
-                if (me && st == QSMD_STATUS_LINEARISABLE)
-                    for (uint32_t d = 0; d < dfs.depth; ++d) L.path[d] = (uint8_t)(dfs.stk.get(d, dfs.depth) & JM);
-            }
-        }
-        if (busy && (fin || st == QSMD_STATUS_SKIPPED)) busy = false;
-    }
-
-    // ---- fold: records up to the best decider
-    int status;
-    uint64_t nodes = 0;
-    if (skipped) {
-        status = QSMD_STATUS_SKIPPED;
-    } else if (timed) {
-        status = QSMD_STATUS_BUDGET;
-        nodes = a.max_nodes;
-    } else if (incomplete || overflow) {
-        status = QSMD_STATUS_HANDED_OFF;
-    } else {
-        uint64_t part = 0;
-        bool ovf = false;
-        for (uint32_t i = lane; i < rec_n; i += 64) {
-            const K rk = rec.get_key(i);
-            if (!best.less(rk)) ovf |= __builtin_add_overflow(part, rec.nodes[i], &part);
-        }
-        const uint64_t sum = wave_sum64(part);
-        ovf |= __ballot(ovf || sum < part) != 0ull;
-        ovf |= __builtin_add_overflow(prefix_sum, sum, &nodes);
-        status = ovf ? QSMD_STATUS_HANDED_OFF : (int)best_status;
-        if (!ovf && a.max_nodes && nodes > a.max_nodes) {
-            status = QSMD_STATUS_BUDGET;
-            nodes = a.max_nodes;
-        }
-    }
-    if (p.stats && lane == 0) {                  // diagnostic
-        unsigned long long* q = p.stats + (uint64_t)blockIdx.x * 8;
-        q[0] += 1;
-        q[1] += tick;
-        q[2] += __builtin_amdgcn_s_memtime() - c0;
-        q[3] += n_splits;
-        q[4] = q[4] > tick ? q[4] : tick;
-        q[7] += nodes;
-    }
-    if (lane == 0) {
-        if (status == QSMD_STATUS_HANDED_OFF) {  // the giant stage searches it again, from the root
-            a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
-        } else {
-            note_failure(a, h, status);
-            a.status[h] = (uint8_t)status;
-            if (a.nodes) a.nodes[h] = nodes;
-            cnt.add(status, nodes);
-        }
-    }
-    if (status == QSMD_STATUS_LINEARISABLE && a.witness && (uint32_t)lane < H.n_ev) {
-        uint8_t* w = a.witness + H.ev_off;
-        if ((uint32_t)lane < best_depth) w[lane] = L.path[lane];
-        else if ((uint32_t)lane == best_depth) w[lane] = QSMD_WITNESS_END;
-    }
-}
-
-// One list (G32: stage 0's heavy histories; G64: stage 0w's): a wavefront
-// takes one history at a time from the queue head.
-template <uint32_t MODEL, class G>
-__device__ __forceinline__ void wave_list(const WaveArgs& p, const uint32_t* list, const uint32_t* count_p,
-                                          uint32_t* head, WaveLds<G>& L, uint32_t* tab, int lane, uint64_t t0,
-                                          Counters& cnt) {
-    using M = typename G::M;
-    const uint32_t count = *count_p;
-    if (count == 0u) return;
-    uint32_t next = 0;
-    if (lane == 0) next = atomicAdd(head, 1u);
-    next = __shfl(next, 0, 64);
-    while (next < count) {
-        const uint32_t g = next;
-        if (lane == 0) next = atomicAdd(head, 1u);      // prefetch the next history
-        const uint32_t h = list[g];
-        const qsmd_hdr H = p.s.hdr[h];
-        // the history once, shared by the lanes: one event per lane
-        if ((uint32_t)lane < H.n_ev) {
-            const uint2 x = p.s.events[H.ev_off + lane];
-            L.hist[lane] = compress<MODEL, G>(x.x, (int32_t)x.y);
-        }
-        // a clear memo (entries of the previous history must not match)
-        for (uint32_t i = (uint32_t)lane * 4u; i < kMemoW * kMemoEntries; i += 256u)
-            *reinterpret_cast<uint4*>(tab + i) = make_uint4(0u, 0u, 0u, 0u);
-        __builtin_amdgcn_wave_barrier();
-        StagedT<M> s{0, 0, 0, 0, 0, true, true, false};
-        finish_shared<G>(L.hist, lane == 0, H.n_ev, H.n_pid, s);
-        __builtin_amdgcn_wave_barrier();
-        if (H.n_ev == 0u || beyond_first_fail(p.s, h)) {   // (stages 0 / 0w never send an empty one)
-            const int st = H.n_ev == 0u ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_SKIPPED;
-            if (lane == 0) {
-                p.s.status[h] = (uint8_t)st;
-                if (p.s.nodes) p.s.nodes[h] = 0;
-                cnt.add(st, 0);
-            }
-        } else if (s.paired) {
-            wave_history<MODEL, M_PAIRED, G>(p, h, H, s, L, tab, lane, t0, cnt);
-        } else {
-            wave_history<MODEL, M_GENERAL, G>(p, h, H, s, L, tab, lane, t0, cnt);
-        }
-        next = __shfl(next, 0, 64);
-    }
-}
-
+// The three lists (stage 0's heavy, stage 0w's heavy, stage 0w's wide), one
+// history per wavefront, grid-stride.
 template <uint32_t MODEL>
 __global__ __launch_bounds__(C_LANES) void wave_search(WaveArgs p) {
-    __shared__ union {
-        WaveLds<G32> g32;
-        WaveLds<G64> g64;
-    } u;
-    __shared__ __attribute__((aligned(16))) uint32_t tab[kMemoW * kMemoEntries];
+    extern __shared__ uint32_t tab[];
     const int lane = threadIdx.x;
+    const uint32_t n32 = *p.count32, n64 = *p.count64, nw = *p.count_wide;
     const uint64_t t0 = p.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     Counters cnt;
-    wave_list<MODEL, G32>(p, p.list32, p.count32, p.next32, u.g32, tab, lane, t0, cnt);
-    wave_list<MODEL, G64>(p, p.list64, p.count64, p.next64, u.g64, tab, lane, t0, cnt);
+    clear_table(tab, p.buckets, lane);
+    uint32_t epoch = 0u, victim = 0u;
+    for (uint32_t i = blockIdx.x; i < n32 + n64 + nw; i += gridDim.x) {
+        const uint32_t h = i < n32 ? p.list32[i] : (i < n32 + n64 ? p.list64[i - n32] : p.list_wide[i - n32 - n64]);
+        const qsmd_hdr H = p.s.hdr[h];
+        const bool wide = i >= n32 + n64;
+        if (wide && (H.n_ev > 128u || H.n_pid > 8u || !p.s.m0_wave)) {   // the giant stage's
+            if (lane == 0) p.s.giant_list[atomicAdd(p.s.giant_count, 1u)] = h;
+            continue;
+        }
+        if (++epoch == kEpochMax) {                  // tags exhausted: clear, start over
+            clear_table(tab, p.buckets, lane);
+            epoch = 1u;
+        }
+        if (H.n_ev <= 64u) wave_history<MODEL, uint64_t>(p, h, H, wide, tab, epoch, victim, lane, t0, cnt);
+        else wave_history<MODEL, M128>(p, h, H, wide, tab, epoch, victim, lane, t0, cnt);
+    }
     cnt.flush(p.s.buckets, lane);
 }
 
 hipError_t launch_wave(const WaveArgs& p, uint32_t grid, hipStream_t s) {
+    const size_t lds = (size_t)p.buckets * 64u * 4u;
     if (p.s.model_id == QSMD_MODEL_BANK)
-        hipLaunchKernelGGL(wave_search<QSMD_MODEL_BANK>, dim3(grid), dim3(C_LANES), 0, s, p);
+        hipLaunchKernelGGL(wave_search<QSMD_MODEL_BANK>, dim3(grid), dim3(C_LANES), lds, s, p);
     else
-        hipLaunchKernelGGL(wave_search<QSMD_MODEL_TICKET>, dim3(grid), dim3(C_LANES), 0, s, p);
+        hipLaunchKernelGGL(wave_search<QSMD_MODEL_TICKET>, dim3(grid), dim3(C_LANES), lds, s, p);
     return hipGetLastError();
 }
 

@@ -95,8 +95,9 @@ def test_random_any_shape(ctx, model):
     _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
 
 
-DEFAULTS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 1, "wave_budget": 16, "wave_max": 16384,
-            "split_budget": 1024, "memo_lane_entries": 256, "memo_grid": 4096, "split_xmemo": 1, "memo_lds": 1}
+DEFAULTS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
+            "wave_grid": 0, "split_budget": 1024, "memo_lane_entries": 256, "memo_grid": 0, "split_xmemo": 1,
+            "memo_lds": 1}
 
 
 @pytest.fixture
@@ -198,19 +199,21 @@ def test_lane_mode(ctx, knobs, name, n, budget, max_nodes, entries, lds):
 
 
 @pytest.mark.parametrize("name,n,budget,max_nodes", LANE_CASES)
-@pytest.mark.parametrize("wave_budget", [1, 4, 16, 64])
-def test_wave_mode(ctx, knobs, name, n, budget, max_nodes, wave_budget):
-    """Wave mode of the heavy stage: one wavefront per history, tasks split
-    to idle lanes after wave_budget nodes (1: a split at nearly every node),
-    the LDS state memo shared by the lanes; max_nodes falls inside reused
-    subtrees and across tasks."""
-    knobs(heavy_mode=0, wave_budget=wave_budget, stage0_budget=budget, stage0w_budget=budget)
+@pytest.mark.parametrize("min_rem,grid", [(4, 0), (0, 0), (64, 0), (0, 7)])
+def test_wave_mode(ctx, knobs, name, n, budget, max_nodes, min_rem, grid):
+    """Wave mode of the heavy stage (csrc/wave.hip): one wavefront per
+    history, the DFS in wave-uniform registers, the exact-count memo in an
+    8-way LDS table per wavefront.  min_rem: memo only above this many
+    remaining events (64: no memo at all, 0: at every node); grid 7: few
+    wavefronts, many histories each (grid-stride, entry tags per history);
+    max_nodes falls inside reused subtrees."""
+    knobs(heavy_mode=0, wave_min_rem=min_rem, wave_grid=grid, stage0_budget=budget, stage0w_budget=budget)
     hdr, ev, _ = gen.generate_config(name, 6, n)
     _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
 
 
 def test_lane_tables_too_large_fall_back_to_wave_mode(ctx, knobs):
-    """Lane-mode tables the device cannot hold keep the context in wave mode:
+    """Lane-mode tables the device cannot hold send the call to wave mode:
     the same results."""
     knobs(heavy_mode=1, memo_grid=65536, memo_lane_entries=65536, stage0_budget=8)
     hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 21, 20000)
@@ -277,7 +280,7 @@ def test_heavy_any_shape(ctx, knobs, model, heavy):
         else:
             hs.append(histgen.wellformed_history(rng, model, rng.randint(6, 16), rng.randint(1, 5)))
     m = models.BY_NAME[model]
-    knobs(heavy_mode=heavy, stage0_budget=4, wave_budget=2)
+    knobs(heavy_mode=heavy, stage0_budget=4, wave_min_rem=0)
     b = codec.encode(m, hs)
     for max_nodes in (0, 50, 3000):
         _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=max_nodes)
@@ -287,8 +290,9 @@ def test_heavy_any_shape(ctx, knobs, model, heavy):
 
 def test_heavy_mode_auto_switches(ctx, knobs):
     """heavy_mode 2 (the default) picks wave or lane mode from the routing of
-    the last finished call; results are exact whichever it picks and across
-    the switches (bug-heavy batch, a clean one, the bug-heavy again)."""
+    the last finished call (lane mode past wave_max heavy histories);
+    results are exact whichever it picks and across the switches (bug-heavy
+    batch, a clean one, the bug-heavy again)."""
     knobs(heavy_mode=2, wave_max=1000)
     b3 = gen.generate_config("bank_4x16_bugs", 11, 30000)
     b2 = gen.generate_config("bank_4x16", 11, 30000)

@@ -283,15 +283,17 @@ def test_stalled_giant_workgroup_reports_budget(ctx):
     first = (hdr[:200].copy(), ev)
     second = (hdr[200:].copy(), ev)
     st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_TICKET, second[0], second[1], threads=8, max_nodes=10**7)
-    ctx.check_arrays(models.MODEL_TICKET, *first, max_nodes=10**7)      # records of another batch
-    ctx.set_time_limit_ms(5)
-    ctx.set_param("giant_stall_us", 100000)
+    ctx.set_param("heavy_mode", 1)          # (lane mode sends every 128-event history to the giant stage)
     try:
+        ctx.check_arrays(models.MODEL_TICKET, *first, max_nodes=10**7)      # records of another batch
+        ctx.set_time_limit_ms(5)
+        ctx.set_param("giant_stall_us", 100000)
         st, nd, _, tot = ctx.check_arrays(models.MODEL_TICKET, *second, max_nodes=10**7)
         assert ctx.timed_out()
     finally:
         ctx.set_param("giant_stall_us", 0)
         ctx.set_time_limit_ms(60000)
+        ctx.set_param("heavy_mode", 2)
     budget = st == codec.STATUS_BUDGET
     assert budget.sum() > 0
     ok = ~budget

@@ -25,10 +25,10 @@ import oracle_c  # noqa: E402
 from qsmd import codec, device, gen, models  # noqa: E402
 
 KNOBS = {"stage0_budget": [0, 4, 16, 32, 40, 64], "stage0w_budget": [0, 4, 32], "heavy_mode": [0, 1, 2],
-         "split_budget": [1, 16, 64, 1024], "memo_lane_entries": [2, 256], "wave_budget": [1, 16],
-         "wave_min_rem": [0, 8], "split_xmemo": [0, 1], "memo_lds": [0, 1, 2]}
-DEFAULT_KNOBS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 1, "split_budget": 1024,
-                 "memo_lane_entries": 256, "wave_budget": 16, "wave_min_rem": 8, "split_xmemo": 1,
+         "split_budget": [1, 16, 64, 1024], "memo_lane_entries": [2, 256], "wave_grid": [0, 5],
+         "wave_min_rem": [0, 4, 64], "split_xmemo": [0, 1], "memo_lds": [0, 1, 2]}
+DEFAULT_KNOBS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 2, "split_budget": 1024,
+                 "memo_lane_entries": 256, "wave_grid": 0, "wave_min_rem": 4, "split_xmemo": 1,
                  "memo_lds": 1}
 
 
