@@ -389,12 +389,18 @@ def main():
     # (6.46-6.54e9 vs 6.28e9 at 40 and 5.81e9 at 20; tools/gpu/ab_params.sh)
     budget0 = args.stage0_budget if args.stage0_budget is not None else (26 if S > 1 else -1)
     knobs = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in args.param]
-    # with calls in flight the heavy stage keeps its memo tables in HBM: the
-    # LDS tables (the library's choice for a short heavy list, best for one
-    # call at a time) take a whole CU per workgroup from the next call's
-    # stage 0 (5.65 vs 5.94e9 histories/s; 3.28 vs 3.07e9 with one call)
-    if S > 1 and "memo_lds" not in dict(knobs):
-        knobs.append(("memo_lds", 0))
+    # with calls in flight the heavy stage runs in lane mode (64 searches per
+    # wavefront: a few dozen wavefronts beside the next call's stage 0) with
+    # its memo tables in HBM (an LDS-table workgroup holds a whole CU).  The
+    # library's default for a short heavy list -- wave mode, one wavefront
+    # per history, the shortest chain for one call at a time -- puts ~2000
+    # wavefronts beside the next stage 0 for ~100 us.
+    # wave_max 0: lane mode once a call has sent any history to the heavy
+    # stage (the first call: wave mode)
+    if S > 1:
+        for k, v in (("memo_lds", 0), ("heavy_mode", 2), ("wave_max", 0)):
+            if k not in dict(knobs):
+                knobs.append((k, v))
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
     run = InFlight(dev, model_id, d_hdr, n, d_ev, len(ev), S, max(1, args.ar_rounds), flags, use_dist, knobs,
                    budget0, streams, host_group)
@@ -453,7 +459,8 @@ def main():
                    "clients": cfg["n_clients"], "ops": cfg["n_ops"],
                    "events_per_history": 2 * cfg["n_ops"], "parallelism": f"shard{world}", "calls_in_flight": S,
                    "stage0_budget": budget0 if budget0 >= 0 else "library default",
-                   "heavy_memo_tables": ("hbm", "lds for short lists", "lds")[dict(knobs).get("memo_lds", 1)],
+                   "heavy_stage": ("lane mode, HBM memo tables" if S > 1 else "library default (wave mode for a "
+                                   "short heavy list)") if not args.param else "knobs: " + ",".join(args.param),
                    "allreduce_every_steps": S * max(1, args.ar_rounds) if use_dist else None,
                    "mode": "memo" if args.memo else "exhaustive"},
         "nodes_per_sec": nodes_total * args.steps / elapsed,

@@ -238,9 +238,10 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *   "giant_grid"        giant stage workgroups (0 = 2 per CU, or 64 when the
  *                       last finished call had no giant history)
  *   "wave_stats_ptr", "memo_stats_ptr", "memo_stats_groups"  diagnostics:
- *                       device buffers: wave mode [max, sum] of DFS
- *                       iterations per history (tools/wave_stats.py), lane
- *                       mode per-group records (tools/memo_stats.py)
+ *                       device buffers: wave mode 5 x u64 (DFS iterations
+ *                       max / sum, s_memtime cycles max / sum, nodes sum per
+ *                       history; tools/wave_stats.py), lane mode per-group
+ *                       records (tools/memo_stats.py)
  *   "giant_stall_us"    diagnostic: the workgroup of the giant stage's first
  *                       frontier chunk starts this late (tests of the time
  *                       limit's phase-wait safety net: a giant combined by a

@@ -385,10 +385,10 @@ static int memo_prepare(qsmd_ctx* c, hipStream_t s, unsigned long long** out) {
 }
 
 // A tail stage's grid: one workgroup per 64 histories the last call sent
-// there, between 2 per CU and `cap` (cap before the first call).
-static uint64_t tail_grid(const qsmd_ctx* c, uint64_t cap, uint64_t last) {
+// there, between `floor` and `cap` (cap before the first call).
+static uint64_t tail_grid(uint64_t floor, uint64_t cap, uint64_t last) {
     if (last == 0xFFFFFFFFull || last > 0xFFFFFFFFull) return cap;
-    return std::min<uint64_t>(cap, std::max<uint64_t>(2ull * c->n_cu, (last + 63) / 64));
+    return std::min<uint64_t>(cap, std::max<uint64_t>(floor, (last + 63) / 64));
 }
 
 // Lane mode's HBM memo tables for a heavy-stage grid of `grid` workgroups
@@ -449,8 +449,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // twice the groups expected -- they would hold CUs the next call's
     // stage 0 could use)
     const uint64_t mg = lt && !wide ? std::min<uint64_t>(c->n_cu, 2 * std::min<uint64_t>(g32, c->n_cu) + 8)
-                                    : tail_grid(c, c->memo_grid ? c->memo_grid : 12ull * c->n_cu,
-                                                c->probe_valid ? heavy_hint : ~0ull);
+                                    : tail_grid(8, c->memo_grid ? c->memo_grid : 12ull * c->n_cu,
+                                                c->probe_valid ? heavy_hint + heavy_hint / 4 : ~0ull);
     if (lane && !(lt && !wide)) lane = lane_tables(c, s, mg);
 
     // ---- workspace: header, lists, giant records, tasks
@@ -530,7 +530,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     aw.heavy_list = h64;
     aw.heavy_count = cnt + C_HEAVY64;
     aw.stage0_budget = c->stage0w_budget ? c->stage0w_budget : ~0ull;
-    HIP_TRY(c, launch_compact64(aw, (uint32_t)tail_grid(c, kStage0wGrid, hint[0]), s), "stage 0w launch");
+    HIP_TRY(c, launch_compact64(aw, (uint32_t)tail_grid(2ull * c->n_cu, kStage0wGrid, hint[0]), s), "stage 0w launch");
     stage_done("stage0w", s, cnt);
     // ---- heavy stage: histories over the stage budgets
     const uint64_t cap = split ? 64 * c->split_budget : 0;
@@ -576,11 +576,14 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         wp.buckets = wide_hint ? 256u : 32u;
         // one workgroup per history the last call sent here (+ 25 %), at
         // least 64 and at most 16 per CU (grid-stride beyond)
+        // the 65..128-event launch when the last call had wide histories
+        wp.wide128 = wide_hint ? 1u : 0u;
         const uint64_t nh = heavy_hint + wide_hint;
         const uint64_t g = c->wave_grid ? c->wave_grid
                          : std::min<uint64_t>(16ull * c->n_cu,
                                               c->probe_valid ? std::max<uint64_t>(64, nh + nh / 4) : 4ull * c->n_cu);
-        HIP_TRY(c, launch_wave(wp, (uint32_t)g, s), "wave launch");
+        const uint64_t g128 = std::min<uint64_t>(16ull * c->n_cu, std::max<uint64_t>(8, wide_hint + wide_hint / 4));
+        HIP_TRY(c, launch_wave(wp, (uint32_t)g, (uint32_t)g128, s), "wave launch");
         stage_done("wave", s, cnt);
     }
     // ---- giant stage: the split search, the combine, (the fixup), the totals

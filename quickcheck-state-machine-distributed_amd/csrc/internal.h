@@ -227,9 +227,10 @@ struct WaveArgs {
     uint32_t memo_min_rem;        // nodes with at most this many events left are not memoised
     uint32_t memo_mode;           // QSMD_FLAG_MEMO: a memo hit counts nothing (explored nodes)
     uint32_t buckets;             // LDS memo table: buckets of 64 words (a power of two)
-    unsigned long long* stats;    // diagnostic: [max, sum] of DFS iterations per history (null in production)
+    uint32_t wide128;             // a second launch searches the wide list's 65..128-event histories
+    unsigned long long* stats;    // diagnostic: DFS iterations [max, sum], s_memtime cycles [max, sum], nodes sum
 };
-hipError_t launch_wave(const WaveArgs& p, uint32_t grid, hipStream_t s);
+hipError_t launch_wave(const WaveArgs& p, uint32_t grid, uint32_t grid128, hipStream_t s);
 
 // memo_search (csrc/memo.hip): per-lane search of a compact stage's heavy
 // histories (s.list / s.list_count) with an exact-count state memo; one

@@ -75,19 +75,10 @@ __device__ __forceinline__ uint32_t mpop(uint64_t m) { return (uint32_t)__builti
 __device__ __forceinline__ uint32_t mpop(const M128& m) {
     return (uint32_t)(__builtin_popcountll(m.lo) + __builtin_popcountll(m.hi));
 }
-__device__ __forceinline__ uint32_t mbitof(uint64_t m, uint32_t j) { return (uint32_t)(m >> j) & 1u; }
-__device__ __forceinline__ uint32_t mbitof(const M128& m, uint32_t j) {
-    return (uint32_t)((j < 64u ? m.lo : m.hi) >> (j & 63u)) & 1u;
-}
 template <typename M> __device__ __forceinline__ M mbit(uint32_t j);
 template <> __device__ __forceinline__ uint64_t mbit<uint64_t>(uint32_t j) { return 1ull << j; }
 template <> __device__ __forceinline__ M128 mbit<M128>(uint32_t j) {
     return mk128(j < 64u ? 1ull << (j & 63u) : 0ull, j < 64u ? 0ull : 1ull << (j & 63u));
-}
-template <typename M> __device__ __forceinline__ M msplat(uint32_t b);
-template <> __device__ __forceinline__ uint64_t msplat<uint64_t>(uint32_t b) { return 0ull - (uint64_t)b; }
-template <> __device__ __forceinline__ M128 msplat<M128>(uint32_t b) {
-    return mk128(0ull - (uint64_t)b, 0ull - (uint64_t)b);
 }
 __device__ __forceinline__ uint64_t mlowest(uint64_t m) { return m & (0ull - m); }
 __device__ __forceinline__ M128 mlowest(const M128& m) { return MaskOps<M128>::lowest(m); }
@@ -114,19 +105,40 @@ template <> struct Geo<M128> { static constexpr uint32_t NW = 2, EW = 16; };
 template <uint32_t MODEL, typename M>
 struct WaveDFS {
     static constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
-    static constexpr uint32_t NW = Geo<M>::NW;
-    M INV, RESP, P0, P1, P2, ALL;
+    static constexpr uint32_t NW = Geo<M>::NW, EW = Geo<M>::EW;
+    M INV, RESP;
     M rem, cand;
     uint64_t nodes;
     uint64_t RS;            // Ticket: levels whose operation was a Reset
     uint32_t depth, ex, neg, found;
-    // lanes: lo / val = event e (lane e % 64 of word e / 64), bal = account q
-    // (lane q), stk = the undo record of level d (lane d: j | ex_a << 7 |
-    // ex_b << 8), ent = the node count at entry of level d (lane d)
-    uint32_t lo[NW];
+    // Bank, for the memo key (kept as the balances change): wacc = accounts
+    // whose balance is beyond i16, mh = XOR of per-account hashes
+    uint32_t wacc, mh;
+    // lanes: lo / val / pidv = event e (lane e % 64 of word e / 64; pidv =
+    // its pid, 0xFF past the history), bal = account q (lane q), kb = the
+    // balances as i16 pairs in the memo key's lane layout (lane l with
+    // l % EW = 4 + q holds accounts 2q, 2q + 1), stk = the undo record of
+    // level d (lane d: j | ex_a << 7 | ex_b << 8), ent = the node count at
+    // entry of level d (lane d)
+    uint32_t lo[NW], pidv[NW];
     int32_t val[NW];
     int32_t bal;
+    uint32_t kb;
     uint32_t stk, ent;
+
+    __device__ static __forceinline__ uint32_t acc_hash(uint32_t c, int32_t v) {
+        return ((uint32_t)v * 0x9E3779B1u) ^ ((c + 1u) * 0x85EBCA77u) ^ ((uint32_t)v >> 7);
+    }
+    // account c := v (old: its balance before), the key parts with it
+    __device__ __forceinline__ void set_bal(uint32_t c, int32_t old, int32_t v) {
+        bal = wli(bal, v, c);
+        const uint32_t w = threadIdx.x % EW, sh = (c & 1u) * 16u;
+        const uint32_t keep = 0xFFFF0000u >> sh;
+        kb = w == 4u + (c >> 1) ? (kb & keep) | (((uint32_t)v & 0xFFFFu) << sh) : kb;
+        const bool fits = v == (int32_t)(int16_t)v;
+        wacc = (wacc & ~(1u << c)) | (fits ? 0u : 1u << c);
+        mh ^= acc_hash(c, old) ^ acc_hash(c, v);
+    }
 
     __device__ __forceinline__ uint32_t ev_lo(uint32_t e) const {
         if constexpr (NW == 1) {
@@ -144,9 +156,11 @@ struct WaveDFS {
             return e < 64u ? x0 : x1;
         }
     }
+    // the events of the pid of event j: one lane compare per event register
     __device__ __forceinline__ M same_pid(uint32_t j) const {
-        const M m0 = msplat<M>(mbitof(P0, j)), m1 = msplat<M>(mbitof(P1, j)), m2 = msplat<M>(mbitof(P2, j));
-        return ~((P0 ^ m0) | (P1 ^ m1) | (P2 ^ m2)) & ALL;
+        const uint32_t p = ev_lo(j) & 0x7Fu;
+        if constexpr (NW == 1) return __ballot(pidv[0] == p);
+        else return mk128(__ballot(pidv[0] == p), __ballot(pidv[1] == p));
     }
 
     // Undo the last level exactly (remaining events, model); returns its candidate.
@@ -166,8 +180,8 @@ struct WaveDFS {
             const int32_t rb = (pb || ia == ib) ? bb - m : 0;      // Transfer's deposit on b undone
             const int32_t cur_a = (tr && ia == ib) ? rb : ba;
             const int32_t ra = pa ? cur_a - bank_sign(code) * m : 0;
-            bal = wli(bal, tr ? rb : bb, ib);                      // a no-op unless Transfer
-            bal = wli(bal, ra, ia);                                // last (ia == ib)
+            if (tr) set_bal(ib, bb, rb);                           // (Transfer only)
+            set_bal(ia, (tr && ia == ib) ? rb : ba, ra);           // last (ia == ib)
             ex = (ex & ~((1u << ia) | ((tr ? 1u : 0u) << ib))) | (pa << ia) | ((tr ? pb : 0u) << ib);
             neg = 0u;   // the parent held the invariant (a step descends only then)
         } else {
@@ -218,8 +232,8 @@ struct WaveDFS {
                 const int32_t na = (ex_a ? bal_a : 0) + (ex_a ? sa : (sa & 1)) * m;
                 const int32_t bo = same ? na : bal_b;
                 const int32_t fb = tr ? (((ex_b != 0u) || same) ? bo : 0) + m : bo;
-                bal = wli(bal, na, ia);
-                bal = wli(bal, fb, ib);
+                set_bal(ia, bal_a, na);
+                if (tr) set_bal(ib, same ? na : bal_b, fb);
                 const int32_t va = same ? fb : na;
                 ex |= ((chk ? 0u : 1u) << ia) | ((tr ? 1u : 0u) << ib);
                 neg = (va | fb) < 0 ? 1u : 0u;
@@ -263,21 +277,20 @@ struct WKey {
 template <uint32_t MODEL, typename M>
 __device__ __forceinline__ WKey wave_key(const WaveDFS<MODEL, M>& d, const SearchArgs& a, uint32_t epoch,
                                          uint32_t bucket_mask, int lane) {
-    uint32_t m[4];
+    constexpr uint32_t EW = Geo<M>::EW;
     bool ok = true;
+    uint32_t mw, mhash;                           // the model: lanes 4..7 (Bank: d.kb), its hash
     if constexpr (MODEL == QSMD_MODEL_BANK) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int32_t b0 = rli(d.bal, 2 * q), b1 = rli(d.bal, 2 * q + 1);
-            ok = ok && b0 == (int32_t)(int16_t)b0 && b1 == (int32_t)(int16_t)b1;
-            m[q] = ((uint32_t)b0 & 0xFFFFu) | ((uint32_t)b1 << 16);
-        }
+        ok = d.wacc == 0u;
+        mw = d.kb;
+        mhash = d.mh;
     } else {
         uint32_t just;
         int32_t n;
         d.ticket_model(a, just, n);
-        m[0] = just | (just ? (uint32_t)n << 1 : 0u);
-        m[1] = m[2] = m[3] = 0u;
+        const uint32_t m0 = just | (just ? (uint32_t)n << 1 : 0u);
+        mw = ((uint32_t)lane % EW) == 4u ? m0 : 0u;
+        mhash = m0 * 0x9E3779B1u;
     }
     uint32_t r0, r1, r2 = 0u, r3 = 0u;
     if constexpr (Geo<M>::NW == 1) {
@@ -290,20 +303,12 @@ __device__ __forceinline__ WKey wave_key(const WaveDFS<MODEL, M>& d, const Searc
         r3 = (uint32_t)(d.rem.hi >> 32);
     }
     const uint32_t w2 = (MODEL == QSMD_MODEL_BANK ? d.ex : 0u) | (epoch << 8);
-    const uint32_t v = (m[0] ^ __builtin_amdgcn_alignbit(m[1], m[1], 8)) ^
-                       (__builtin_amdgcn_alignbit(m[2], m[2], 16) ^ __builtin_amdgcn_alignbit(m[3], m[3], 24));
-    uint32_t hsh = (r0 * 0x9E3779B1u) ^ ((r1 ^ w2) * 0x85EBCA77u) ^ (v * 0xC2B2AE3Du) ^
-                   ((r2 ^ __builtin_amdgcn_alignbit(r3, r3, 16)) * 0x27D4EB2Fu);
+    uint32_t hsh = (r0 * 0x9E3779B1u) ^ ((r1 ^ w2) * 0x85EBCA77u) ^ mhash ^ ((r2 ^ (r3 << 16 | r3 >> 16)) * 0x27D4EB2Fu);
     hsh ^= (hsh >> 16) ^ (hsh >> 24);
-    const uint32_t w = (uint32_t)lane & (Geo<M>::EW - 1u);
-    uint32_t x = w == 0u ? r0 : 0u;
-    x = w == 1u ? r1 : x;
-    x = w == 2u ? w2 : x;
-    x = w == 4u ? m[0] : x;
-    x = w == 5u ? m[1] : x;
-    x = w == 6u ? m[2] : x;
-    x = w == 7u ? m[3] : x;
-    if constexpr (Geo<M>::EW == 16) {
+    const uint32_t w = (uint32_t)lane % EW;
+    uint32_t x = w == 0u ? r0 : (w == 1u ? r1 : (w == 2u ? w2 : 0u));
+    x = (w >= 4u && w < 8u) ? mw : x;
+    if constexpr (EW == 16) {
         x = w == 8u ? r2 : x;
         x = w == 9u ? r3 : x;
     }
@@ -346,7 +351,7 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
     WaveDFS<MODEL, M> d;
     // staging: lane l loads events l (and l + 64): coalesced 8-B loads
     bool bad = false, big = false;
-    uint64_t bl[NW][6];            // ballots: RESP, P0, P1, P2, ALL, (unused)
+    uint64_t resp[NW], all[NW];
 #pragma unroll
     for (uint32_t w = 0; w < NW; ++w) {
         const uint32_t e = (uint32_t)lane + 64u * w;
@@ -355,25 +360,22 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
         d.lo[w] = x.x;
         d.val[w] = (int32_t)x.y;
         const uint32_t pid = x.x & 0x7Fu;
+        d.pidv[w] = in ? pid : 0xFFu;
         bad = bad || (in && (!valid_bits<MODEL>(x.x) || pid >= H.n_pid));
         big = big || (in && (x.x & 0x80u) == 0u && ((int32_t)x.y >= kWideValue || (int32_t)x.y <= -kWideValue));
-        bl[w][0] = __ballot(in && (x.x & 0x80u));
-        bl[w][1] = __ballot(in && (pid & 1u));
-        bl[w][2] = __ballot(in && (pid & 2u));
-        bl[w][3] = __ballot(in && (pid & 4u));
-        bl[w][4] = __ballot(in);
+        resp[w] = __ballot(in && (x.x & 0x80u));
+        all[w] = __ballot(in);
     }
+    M ALL;
     if constexpr (NW == 1) {
-        d.RESP = bl[0][0]; d.P0 = bl[0][1]; d.P1 = bl[0][2]; d.P2 = bl[0][3]; d.ALL = bl[0][4];
+        d.RESP = resp[0];
+        ALL = all[0];
     } else {
-        d.RESP = mk128(bl[0][0], bl[1][0]);
-        d.P0 = mk128(bl[0][1], bl[1][1]);
-        d.P1 = mk128(bl[0][2], bl[1][2]);
-        d.P2 = mk128(bl[0][3], bl[1][3]);
-        d.ALL = mk128(bl[0][4], bl[1][4]);
+        d.RESP = mk128(resp[0], resp[1]);
+        ALL = mk128(all[0], all[1]);
     }
-    d.INV = d.ALL & ~d.RESP;
-    d.rem = d.ALL;
+    d.INV = ALL & ~d.RESP;
+    d.rem = ALL;
     d.cand = mcands(d.rem, d.INV, d.RESP);
     d.depth = 0u;
     d.found = 0u;
@@ -383,8 +385,17 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
     d.ent = 0u;
     d.ex = a.m0_exists;
     const bool e_q = (uint32_t)lane < QSMD_BANK_MAX_ACCOUNTS && ((a.m0_exists >> (uint32_t)lane) & 1u);
-    d.bal = e_q ? (int32_t)a.m0_val[lane & 7] : 0;
-    d.neg = __ballot(e_q && d.bal < 0) != 0ull ? 1u : 0u;
+    d.bal = 0;
+    d.neg = __ballot(e_q && (int32_t)a.m0_val[lane & 7] < 0) != 0ull ? 1u : 0u;
+    d.kb = 0u;
+    d.wacc = 0u;
+    d.mh = 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < QSMD_BANK_MAX_ACCOUNTS; ++q) {
+        d.mh ^= WaveDFS<MODEL, M>::acc_hash(q, 0);
+        if constexpr (MODEL == QSMD_MODEL_BANK)
+            if ((a.m0_exists >> q) & 1u) d.set_bal(q, 0, (int32_t)a.m0_val[q]);
+    }
 
     int status = -1;
     if (__ballot(bad) != 0ull) {
@@ -397,10 +408,11 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
         status = QSMD_STATUS_SKIPPED;
     }
     bool skip = false;
-    uint64_t iter = 0;
+    uint32_t iter = 0;
+    const uint64_t c0 = p.stats ? __builtin_amdgcn_s_memtime() : 0ull;
     const uint32_t min_rem = p.memo_min_rem;
     const bool counts = !p.memo_mode;            // exact counts (else QSMD_FLAG_MEMO: explored nodes)
-    const uint64_t cap = wide ? p.explore_cap_wide : p.explore_cap;
+    const uint32_t cap = (uint32_t)min(wide ? p.explore_cap_wide : p.explore_cap, 0xFFFFFFFFull);
     while (status < 0) {
         const bool empty = !mnz(d.cand);
         if (empty && (d.found == 0u || d.depth == 0u)) {
@@ -457,8 +469,12 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
         }
     }
     if (p.stats && lane == 0) {
+        const uint64_t cyc = __builtin_amdgcn_s_memtime() - c0;
         atomicMax(p.stats + 0, (unsigned long long)iter);
         atomicAdd(p.stats + 1, (unsigned long long)iter);
+        atomicMax(p.stats + 2, (unsigned long long)cyc);
+        atomicAdd(p.stats + 3, (unsigned long long)cyc);
+        atomicAdd(p.stats + 4, (unsigned long long)d.nodes);
     }
     if (status == QSMD_STATUS_HANDED_OFF) {          // the giant stage searches it (exact, from the root)
         if (lane == 0) a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
@@ -484,12 +500,17 @@ __device__ __forceinline__ void clear_table(uint32_t* tab, uint32_t buckets, int
 }  // namespace
 
 // The three lists (stage 0's heavy, stage 0w's heavy, stage 0w's wide), one
-// history per wavefront, grid-stride.
-template <uint32_t MODEL>
+// history per wavefront, grid-stride; two kernels so that each holds one mask
+// width in its scalar registers: u64 (list32, list64 and the wide list's
+// histories of <= 64 events) and, when p.wide128, M128 (the wide list's
+// 65..128-event histories).  A wide history neither takes (> 128 events, > 8
+// pids, model0 values beyond +-2^24) goes to the giant stage, once.
+template <uint32_t MODEL, typename M>
 __global__ __launch_bounds__(C_LANES) void wave_search(WaveArgs p) {
+    constexpr bool W128 = Geo<M>::NW == 2;
     extern __shared__ uint32_t tab[];
     const int lane = threadIdx.x;
-    const uint32_t n32 = *p.count32, n64 = *p.count64, nw = *p.count_wide;
+    const uint32_t n32 = W128 ? 0u : *p.count32, n64 = W128 ? 0u : *p.count64, nw = *p.count_wide;
     const uint64_t t0 = p.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     Counters cnt;
     clear_table(tab, p.buckets, lane);
@@ -498,26 +519,36 @@ __global__ __launch_bounds__(C_LANES) void wave_search(WaveArgs p) {
         const uint32_t h = i < n32 ? p.list32[i] : (i < n32 + n64 ? p.list64[i - n32] : p.list_wide[i - n32 - n64]);
         const qsmd_hdr H = p.s.hdr[h];
         const bool wide = i >= n32 + n64;
-        if (wide && (H.n_ev > 128u || H.n_pid > 8u || !p.s.m0_wave)) {   // the giant stage's
-            if (lane == 0) p.s.giant_list[atomicAdd(p.s.giant_count, 1u)] = h;
-            continue;
+        if (wide) {
+            const bool mine = W128 ? H.n_ev > 64u : (H.n_ev <= 64u || !p.wide128);
+            if (!mine) continue;
+            if (H.n_ev > (W128 || !p.wide128 ? 128u : 64u) || H.n_ev > 64u * Geo<M>::NW || H.n_pid > 8u ||
+                !p.s.m0_wave) {                  // the giant stage's
+                if (lane == 0) p.s.giant_list[atomicAdd(p.s.giant_count, 1u)] = h;
+                continue;
+            }
         }
         if (++epoch == kEpochMax) {                  // tags exhausted: clear, start over
             clear_table(tab, p.buckets, lane);
             epoch = 1u;
         }
-        if (H.n_ev <= 64u) wave_history<MODEL, uint64_t>(p, h, H, wide, tab, epoch, victim, lane, t0, cnt);
-        else wave_history<MODEL, M128>(p, h, H, wide, tab, epoch, victim, lane, t0, cnt);
+        wave_history<MODEL, M>(p, h, H, wide, tab, epoch, victim, lane, t0, cnt);
     }
     cnt.flush(p.s.buckets, lane);
 }
 
-hipError_t launch_wave(const WaveArgs& p, uint32_t grid, hipStream_t s) {
+hipError_t launch_wave(const WaveArgs& p, uint32_t grid, uint32_t grid128, hipStream_t s) {
     const size_t lds = (size_t)p.buckets * 64u * 4u;
     if (p.s.model_id == QSMD_MODEL_BANK)
-        hipLaunchKernelGGL(wave_search<QSMD_MODEL_BANK>, dim3(grid), dim3(C_LANES), lds, s, p);
+        hipLaunchKernelGGL((wave_search<QSMD_MODEL_BANK, uint64_t>), dim3(grid), dim3(C_LANES), lds, s, p);
     else
-        hipLaunchKernelGGL(wave_search<QSMD_MODEL_TICKET>, dim3(grid), dim3(C_LANES), lds, s, p);
+        hipLaunchKernelGGL((wave_search<QSMD_MODEL_TICKET, uint64_t>), dim3(grid), dim3(C_LANES), lds, s, p);
+    if (p.wide128) {
+        if (p.s.model_id == QSMD_MODEL_BANK)
+            hipLaunchKernelGGL((wave_search<QSMD_MODEL_BANK, M128>), dim3(grid128), dim3(C_LANES), lds, s, p);
+        else
+            hipLaunchKernelGGL((wave_search<QSMD_MODEL_TICKET, M128>), dim3(grid128), dim3(C_LANES), lds, s, p);
+    }
     return hipGetLastError();
 }
 

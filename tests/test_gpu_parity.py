@@ -14,7 +14,7 @@ import pytest
 import histgen
 import oracle_c
 from kats import KATS
-from qsmd import codec, gen, models
+from qsmd import codec, device, gen, models
 from qsmd.linearisability import linearisable, linearisable_batch, replay_witness
 
 pytestmark = pytest.mark.gpu

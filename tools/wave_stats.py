@@ -22,7 +22,7 @@ def main():
     for k, v in params.items():
         ctx.set_param(k, int(v))
     dev = torch.device("cuda:0")
-    stats = torch.zeros(2, dtype=torch.int64, device=dev)
+    stats = torch.zeros(5, dtype=torch.int64, device=dev)
     ctx.set_param("wave_stats_ptr", stats.data_ptr())
     hdr, ev, _ = gen.generate_config(name, 0, n, threads=16)
     d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
@@ -41,7 +41,9 @@ def main():
         heavy = probe["heavy32"] + probe["heavy64"]
         s0, call = ctx.timing_read()
         print(f"call {i}: device {call[0]:.3f} ms (stage 0 {s0[0]:.3f}); heavy histories {heavy}, "
-              f"DFS iterations max {q[0]}, mean {q[1] / max(heavy, 1):.1f}", flush=True)
+              f"DFS iterations max {q[0]}, mean {q[1] / max(heavy, 1):.1f}; cycles per history max {q[2]}, "
+              f"mean {q[3] / max(heavy, 1):.0f}; cycles per iteration {q[3] / max(q[1], 1):.0f}; "
+              f"nodes per history {q[4] / max(heavy, 1):.1f}", flush=True)
     ctx.set_param("wave_stats_ptr", 0)
     ctx.close()
 
