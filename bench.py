@@ -394,11 +394,9 @@ def main():
     # its memo tables in HBM (an LDS-table workgroup holds a whole CU).  The
     # library's default for a short heavy list -- wave mode, one wavefront
     # per history, the shortest chain for one call at a time -- puts ~2000
-    # wavefronts beside the next stage 0 for ~100 us.
-    # wave_max 0: lane mode once a call has sent any history to the heavy
-    # stage (the first call: wave mode)
+    # wavefronts beside the next stage 0 for ~100 us
     if S > 1:
-        for k, v in (("memo_lds", 0), ("heavy_mode", 2), ("wave_max", 0)):
+        for k, v in (("memo_lds", 0), ("heavy_mode", 1)):
             if k not in dict(knobs):
                 knobs.append((k, v))
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)

@@ -74,7 +74,7 @@ struct qsmd_ctx {
     uint32_t* debug_host = nullptr;    // QSMD_SYNC_STAGES: giant-stage heartbeat (pinned)
     // lane mode's tables: one per lane slot of the memo grid
     uint64_t memo_grid = 0;            // heavy stage (lane mode): workgroups at most (0 = 12 per CU); one table each
-    uint64_t mt_entries = 256;
+    uint64_t mt_entries = 128;
     char* mt = nullptr;
     size_t mt_bytes = 0;
     uint32_t mt_epoch = 0;
@@ -449,8 +449,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // twice the groups expected -- they would hold CUs the next call's
     // stage 0 could use)
     const uint64_t mg = lt && !wide ? std::min<uint64_t>(c->n_cu, 2 * std::min<uint64_t>(g32, c->n_cu) + 8)
-                                    : tail_grid(8, c->memo_grid ? c->memo_grid : 12ull * c->n_cu,
-                                                c->probe_valid ? heavy_hint + heavy_hint / 4 : ~0ull);
+                                    : (c->probe_valid ? tail_grid(8, c->memo_grid ? c->memo_grid : 12ull * c->n_cu,
+                                                                  heavy_hint + heavy_hint / 4)
+                                                      : (uint64_t)c->n_cu);   // (no hint: grid-stride)
     if (lane && !(lt && !wide)) lane = lane_tables(c, s, mg);
 
     // ---- workspace: header, lists, giant records, tasks

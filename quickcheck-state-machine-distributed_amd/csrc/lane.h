@@ -8,6 +8,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "internal.h"
 #include "models.h"
 
@@ -127,30 +129,35 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 }
 
 // include/qsmd.h encoding rules, branch-free (the pid range is checked
-// against the header's n_pid by finish_lane).
+// against the header's n_pid by finish_lane).  As bit tests on the event's
+// lo word (kp | code << 8 | a << 16 | b << 24): pid < 8 = bits 3-6 clear;
+// Ticket code <= 1 = bits 9-15 clear; Bank response code <= 7 = bits 11-15
+// clear; Bank request code <= 4, account a < 8 = bits 19-23 clear, and for a
+// Transfer b < 8 = bits 27-31 clear.
 template <uint32_t MODEL>
 __device__ __forceinline__ bool valid_bits(uint32_t lo) {
-    const uint32_t c = (lo >> 8) & 0xFFu, ea = (lo >> 16) & 0xFFu, eb = lo >> 24;
-    const bool pid_ok = (lo & 0x78u) == 0u;                 // pid < 8
     if constexpr (MODEL == QSMD_MODEL_TICKET) {
-        return pid_ok & (c <= 1u);
+        return (lo & 0xFE78u) == 0u;
     } else {
+        // a request is bad when (code << 5 | b >> 3) > (Transfer << 5): code > 4,
+        // or a Transfer with b >= 8
         const bool resp = (lo & 0x80u) != 0u;
-        const bool inv_ok = (c <= QSMD_BANK_TRANSFER) & (ea < 8u) & ((c != QSMD_BANK_TRANSFER) | (eb < 8u));
-        return pid_ok & (resp ? (c <= QSMD_BANK_BALANCE) : inv_ok);
+        const uint32_t bits = lo & (resp ? 0xF878u : 0x00F80078u);
+        const uint32_t req = resp ? 0u : ((((lo >> 8) & 0xFFu) << 5) | (lo >> 27));
+        return (bits | (req > (QSMD_BANK_TRANSFER << 5) ? 1u : 0u)) == 0u;
     }
 }
 
 // The compressed word of one event, or a marker (MARK_BAD / MARK_WIDE).
+// A value fits when the word's value field sign-extends back to it.
 template <uint32_t MODEL, class G = G32>
 __device__ __forceinline__ uint32_t compress(uint32_t lo, int32_t val) {
     const bool resp = (lo & 0x80u) != 0u;
-    const uint32_t head = (lo & 7u) | ((lo >> 4) & 8u) | ((lo >> 4) & 0x70u);   // pid | resp | code
+    const uint32_t head = (lo & 7u) | ((lo >> 4) & 0x78u);                      // pid | resp | code
     const uint32_t inv = head | ((lo >> 9) & 0x380u) | ((lo >> 14) & 0x1C00u) | ((uint32_t)val << (32 - G::IVB));
     const uint32_t rsp = head | ((uint32_t)val << (32 - RVAL_BITS));
-    const int32_t half = resp ? (1 << (RVAL_BITS - 1)) : (1 << (G::IVB - 1));
-    const bool fit = (uint32_t)(val + half) < (uint32_t)(2 * half);
     const uint32_t w = resp ? rsp : inv;
+    const bool fit = ((int32_t)w >> (resp ? 32 - RVAL_BITS : 32 - G::IVB)) == val;
     return !valid_bits<MODEL>(lo) ? MARK_BAD : (fit ? w : MARK_WIDE);
 }
 
@@ -260,39 +267,54 @@ __device__ __forceinline__ void stage_packed_body(const SearchArgs& a, uint32_t 
     if (((off0 | total_ev) & 1u) == 0u) {         // 16-B aligned start, whole 16-B pairs
         const uint4* blk = reinterpret_cast<const uint4*>(a.events + off0);
         const uint32_t nq = total_ev / 2u;
-        for (uint32_t k0 = 0; k0 < nq; k0 += U * 64u) {
+        // U x 64 pairs per step: full steps without per-element guards, then the rest
+        auto step = [&](uint32_t k0, auto guard) {
+            constexpr bool GUARD = decltype(guard)::value;
             uint4 x[U];
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
                 const uint32_t q = k0 + u * 64u + (uint32_t)lane;
-                x[u] = q < nq ? blk[q] : make_uint4(0u, 0u, 0u, 0u);
+                x[u] = (!GUARD || q < nq) ? blk[q] : make_uint4(0u, 0u, 0u, 0u);
             }
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
                 const uint32_t q = k0 + u * 64u + (uint32_t)lane;
                 uint32_t e0, e1;
-                const uint32_t c0 = col_of(2u * q, e0), c1 = col_of(2u * q + 1u, e1);
-                if (2u * q < total_ev) s_ev[e0][c0] = compress<MODEL, G>(x[u].x, (int32_t)x[u].y);
-                if (2u * q + 1u < total_ev) s_ev[e1][c1] = compress<MODEL, G>(x[u].z, (int32_t)x[u].w);
+                const uint32_t c0 = col_of(2u * q, e0);
+                // an even power-of-two length: both events of the pair in one
+                // history (one ds_write2 per pair)
+                const uint32_t c1 = POW2 ? c0 : col_of(2u * q + 1u, e1);
+                if (POW2) e1 = e0 + 1u;
+                if (!GUARD || q < nq) {
+                    s_ev[e0][c0] = compress<MODEL, G>(x[u].x, (int32_t)x[u].y);
+                    s_ev[e1][c1] = compress<MODEL, G>(x[u].z, (int32_t)x[u].w);
+                }
             }
-        }
+        };
+        uint32_t k0 = 0;
+        for (; k0 + U * 64u <= nq; k0 += U * 64u) step(k0, std::false_type{});
+        if (k0 < nq) step(k0, std::true_type{});
     } else {
         const uint2* blk = a.events + off0;
-        for (uint32_t k0 = 0; k0 < total_ev; k0 += 2u * U * 64u) {
+        auto step = [&](uint32_t k0, auto guard) {
+            constexpr bool GUARD = decltype(guard)::value;
             uint2 x[2u * U];
 #pragma unroll
             for (uint32_t u = 0; u < 2u * U; ++u) {
                 const uint32_t g = k0 + u * 64u + (uint32_t)lane;
-                x[u] = g < total_ev ? blk[g] : make_uint2(0u, 0u);
+                x[u] = (!GUARD || g < total_ev) ? blk[g] : make_uint2(0u, 0u);
             }
 #pragma unroll
             for (uint32_t u = 0; u < 2u * U; ++u) {
                 const uint32_t g = k0 + u * 64u + (uint32_t)lane;
                 uint32_t e;
                 const uint32_t c = col_of(g, e);
-                if (g < total_ev) s_ev[e][c] = compress<MODEL, G>(x[u].x, (int32_t)x[u].y);
+                if (!GUARD || g < total_ev) s_ev[e][c] = compress<MODEL, G>(x[u].x, (int32_t)x[u].y);
             }
-        }
+        };
+        uint32_t k0 = 0;
+        for (; k0 + 2u * U * 64u <= total_ev; k0 += 2u * U * 64u) step(k0, std::false_type{});
+        if (k0 < total_ev) step(k0, std::true_type{});
     }
 }
 
@@ -301,7 +323,7 @@ __device__ __forceinline__ void stage_packed_body(const SearchArgs& a, uint32_t 
 template <uint32_t MODEL, class G = G32>
 __device__ __forceinline__ void stage_packed(const SearchArgs& a, uint32_t N0, uint32_t off0, uint32_t nh,
                                              uint32_t (*s_ev)[C_LANES], int lane) {
-    if ((N0 & (N0 - 1u)) == 0u) stage_packed_body<MODEL, G, true>(a, N0, off0, nh, s_ev, lane);
+    if ((N0 & (N0 - 1u)) == 0u && N0 >= 2u) stage_packed_body<MODEL, G, true>(a, N0, off0, nh, s_ev, lane);
     else stage_packed_body<MODEL, G, false>(a, N0, off0, nh, s_ev, lane);
 }
 

@@ -96,7 +96,7 @@ def test_random_any_shape(ctx, model):
 
 
 DEFAULTS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
-            "wave_grid": 0, "split_budget": 1024, "memo_lane_entries": 256, "memo_grid": 0, "split_xmemo": 1,
+            "wave_grid": 0, "split_budget": 1024, "memo_lane_entries": 128, "memo_grid": 0, "split_xmemo": 1,
             "memo_lds": 1}
 
 
