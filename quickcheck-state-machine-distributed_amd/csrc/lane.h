@@ -349,22 +349,43 @@ __device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane,
         n_max = __ballot(n_cl >= t) ? t : n_max;
     }
     const M ALL = mask_below(n_ev, (M)0);
-    M RESP = 0, P0 = 0, P1 = 0, P2 = 0, BAD = 0, WIDE = 0;
+    // Per 8 events: their low nibbles (pid bits 0-2, resp bit 3) packed 4
+    // bits apart, then split into the 4 bit planes by shifts (8 bits each);
+    // the marker test (an invocation with code 6 or 7: bits 5 and 6 set, bit
+    // 3 clear) as one bit per event.  BAD / WIDE apart only when some lane
+    // of the wavefront has a marker (injected inputs; never in a clean batch).
+    M RESP = 0, P0 = 0, P1 = 0, P2 = 0, MK = 0;
+    auto plane8 = [](uint32_t nib, uint32_t b) {   // bits b, b+4, ..., b+28 -> bits 0..7
+        uint32_t t = (nib >> b) & 0x11111111u;
+        t = (t | (t >> 3)) & 0x03030303u;
+        t = (t | (t >> 6)) & 0x000F000Fu;
+        return (t | (t >> 12)) & 0xFFu;
+    };
 #pragma unroll 1
     for (uint32_t c0 = 0; c0 < n_max; c0 += U) {
         uint32_t W[U];
 #pragma unroll
         for (uint32_t k = 0; k < U; ++k) W[k] = s_ev[c0 + k][lane];
+        uint32_t nib = 0u, mk = 0u;
 #pragma unroll
         for (uint32_t k = 0; k < U; ++k) {
-            const uint32_t e = c0 + k, w = W[k];
-            RESP |= (M)((w >> 3) & 1u) << e;
-            P0 |= (M)(w & 1u) << e;
-            P1 |= (M)((w >> 1) & 1u) << e;
-            P2 |= (M)((w >> 2) & 1u) << e;
-            const uint32_t mk = w & 0x78u;
-            BAD |= (M)(mk == MARK_BAD ? 1u : 0u) << e;
-            WIDE |= (M)(mk == MARK_WIDE ? 1u : 0u) << e;
+            const uint32_t w = W[k];
+            nib |= (w & 0xFu) << (4u * k);
+            mk |= ((w & (w << 1) & ~(w << 3)) >> 6 & 1u) << k;
+        }
+        RESP |= (M)plane8(nib, 3) << c0;
+        P0 |= (M)plane8(nib, 0) << c0;
+        P1 |= (M)plane8(nib, 1) << c0;
+        P2 |= (M)plane8(nib, 2) << c0;
+        MK |= (M)mk << c0;
+    }
+    M BAD = 0, WIDE = 0;
+    if (__ballot((MK & ALL) != (M)0)) {
+#pragma unroll 1
+        for (uint32_t e = 0; e < n_max; ++e) {
+            const uint32_t mkw = s_ev[e][lane] & 0x78u;
+            BAD |= (M)(mkw == MARK_BAD ? 1u : 0u) << e;
+            WIDE |= (M)(mkw == MARK_WIDE ? 1u : 0u) << e;
         }
     }
     RESP &= ALL;
