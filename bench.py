@@ -134,7 +134,21 @@ class InFlight:
                 self._allreduce(((self.k - 1) // self.B) % 2)
             self.k = (self.k + self.B - 1) // self.B * self.B
 
+    def prime(self):
+        """One call per context before the warm-up, synchronised: the library
+        sizes a context's lane-mode memo tables from its last finished call's
+        heavy count (api.hip), so each context's second call may grow them
+        (hipMalloc + clear); priming makes that happen outside the steps."""
+        for i in range(self.S):
+            d_st, d_nd = self.outs[i]
+            with torch.cuda.stream(self.streams[i]):
+                self.ctxs[i].check_device(self.model_id, self.d_hdr.data_ptr(), self.n, self.d_ev.data_ptr(),
+                                          self.n_ev, d_st.data_ptr(), d_nd.data_ptr(), None, None, flags=self.flags,
+                                          stream=self.streams[i].cuda_stream)
+        torch.cuda.synchronize(self.dev)
+
     def timed(self, steps, warmup):
+        self.prime()
         for _ in range(warmup):
             self.step()
         self.drain()

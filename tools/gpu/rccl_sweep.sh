@@ -6,7 +6,7 @@
 set -o pipefail
 R=${1:-3}; shift
 mkdir -p gpurun_out/rccl
-rm -f gpurun_out/rccl/*
+rm -f gpurun_out/rccl/*.json gpurun_out/rccl/*.err
 for spec in "$@"; do
   IFS='|' read -r tag envs args <<< "$spec"
   for r in $(seq 1 "$R"); do
