@@ -235,12 +235,18 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *                       + 25 %, at most 16 per CU; grid-stride beyond)
  *   "wave_min_rem"      wave mode: no memo probe at nodes with at most this
  *                       many remaining events (default 4)
+ *   "dag_states"        wave mode: capacity in states of the per-wavefront
+ *                       state DAG (default 128, items 4x that; 0 = the DFS
+ *                       for every history); a history whose DAG does not fit
+ *                       runs the DFS
  *   "giant_grid"        giant stage workgroups (0 = 2 per CU, or 64 when the
  *                       last finished call had no giant history)
  *   "wave_stats_ptr", "memo_stats_ptr", "memo_stats_groups"  diagnostics:
- *                       device buffers: wave mode 5 x u64 (DFS iterations
+ *                       device buffers: wave mode 16 x u64 (DFS iterations
  *                       max / sum, s_memtime cycles max / sum, nodes sum per
- *                       history; tools/wave_stats.py), lane mode per-group
+ *                       DFS-searched history; DAG-searched histories, their
+ *                       cycles max / sum, per-phase cycles, levels;
+ *                       tools/wave_stats.py), lane mode per-group
  *                       records (tools/memo_stats.py)
  *   "giant_stall_us"    diagnostic: the workgroup of the giant stage's first
  *                       frontier chunk starts this late (tests of the time

@@ -36,9 +36,12 @@ struct qsmd_ctx {
     char* ws = nullptr;
     size_t ws_bytes = 0;
     bool ws_dirty = true;              // the header must be restored before the next call
-    // staging for the host-memory entry point (device)
+    // staging for the host-memory entry point: device buffer and its pinned
+    // host mirror (one copy in, one copy out per call)
     char* io = nullptr;
     size_t io_bytes = 0;
+    char* pin = nullptr;
+    size_t pin_bytes = 0;
     // the calls of this context are ordered: each waits for the previous one
     // (whatever its stream), and buffers are freed only once it is done
     hipEvent_t done_ev = nullptr;
@@ -58,7 +61,10 @@ struct qsmd_ctx {
     uint64_t split_budget = 1024;      // giant stage: whole-search iterations = 16x, heavy-stage cap = 64x
     uint64_t wave_grid = 0;            // heavy stage, wave mode: workgroups (0 = from the last call's heavy count)
     uint64_t wave_min_rem = 4;         // heavy stage, wave mode: nodes with at most this many events left skip the memo
-    unsigned long long* wave_stats = nullptr;   // diagnostic (wave_stats_ptr): 2 x u64 (max, sum of DFS iterations)
+    uint64_t dag_states = 128;         // heavy stage, wave mode: state-DAG capacity per wavefront (0 = DFS only)
+    uint32_t* dag_dbg = nullptr;       // diagnostic (dag_debug_ptr / dag_debug_hist)
+    uint64_t dag_dbg_h = 0;
+    unsigned long long* wave_stats = nullptr;   // diagnostic (wave_stats_ptr): 16 x u64 (include/qsmd.h)
     unsigned long long* memo_stats = nullptr;   // diagnostic (memo_stats_ptr): 8 x u64 per heavy-stage group
     uint64_t memo_stats_groups = 0;             // (memo_stats_groups)
     uint32_t memo_lds = 1;                      // heavy-stage memo tables in LDS: 0 never, 1 short lists, 2 always
@@ -87,6 +93,7 @@ struct qsmd_ctx {
     unsigned long long* memo = nullptr;
     uint64_t memo_entries = 1ull << 22;
     uint64_t memo_alloc = 0;
+    uint32_t memo_epoch = 0;
     // split-search entry points: their own device buffers
     char* sx = nullptr;
     size_t sx_bytes = 0;
@@ -260,6 +267,7 @@ void qsmd_close(qsmd_ctx* c) {
     if (c->xm) (void)hipFree(c->xm);
     if (c->memo) (void)hipFree(c->memo);
     if (c->io) (void)hipFree(c->io);
+    if (c->pin) (void)hipHostFree(c->pin);
     for (auto e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -300,9 +308,16 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "giant_stall_us") {     // diagnostic (tests of the phase-wait safety net)
         if (value > 10000000ull) return fail(c, QSMD_ERR_ARG, "giant_stall_us in 0..10^7");
         c->giant_stall_us = value;
+    } else if (n == "dag_states") {
+        if (value > 4095) return fail(c, QSMD_ERR_ARG, "dag_states in 0..4095 (0 = the DFS only)");
+        c->dag_states = value;
+    } else if (n == "dag_debug_ptr") {      // diagnostic: device buffer (16 + DAG LDS words) for one history
+        c->dag_dbg = reinterpret_cast<uint32_t*>(value);
+    } else if (n == "dag_debug_hist") {
+        c->dag_dbg_h = value;
     } else if (n == "wave_min_rem") {
         c->wave_min_rem = std::min<uint64_t>(value, 0xFFFFFFFFull);
-    } else if (n == "wave_stats_ptr") {     // diagnostic: device buffer of 2 x u64 (zeroed by the caller)
+    } else if (n == "wave_stats_ptr") {     // diagnostic: device buffer of 16 x u64 (zeroed by the caller)
         c->wave_stats = reinterpret_cast<unsigned long long*>(value);
     } else if (n == "memo_stats_ptr") {     // diagnostic: device buffer of 8 x u64 per heavy-stage group (zeroed)
         c->memo_stats = reinterpret_cast<unsigned long long*>(value);
@@ -365,8 +380,10 @@ int qsmd_set_time_limit_ms(qsmd_ctx* c, uint64_t ms) {
     return QSMD_OK;
 }
 
-// The QSMD_FLAG_MEMO table, cleared for this call (entries are only valid within one).
-static int memo_prepare(qsmd_ctx* c, hipStream_t s, unsigned long long** out) {
+// The QSMD_FLAG_MEMO table and this call's epoch (entries are only valid
+// within one call: an entry of another epoch counts as empty, so the table is
+// cleared when allocated and when the 24-bit epochs wrap, not per call).
+static int memo_prepare(qsmd_ctx* c, hipStream_t s, unsigned long long** out, uint32_t* epoch) {
     if (c->memo_alloc != c->memo_entries) {
         if (c->memo) {
             quiesce(c);
@@ -378,9 +395,14 @@ static int memo_prepare(qsmd_ctx* c, hipStream_t s, unsigned long long** out) {
         hipError_t e = hipMalloc(reinterpret_cast<void**>(&c->memo), c->memo_entries * 64);
         if (e != hipSuccess) return fail(c, QSMD_ERR_NOMEM, "hipMalloc memo table", e);
         c->memo_alloc = c->memo_entries;
+        HIP_TRY(c, hipMemsetAsync(c->memo, 0, c->memo_alloc * 64, s), "memset memo table");
     }
-    HIP_TRY(c, hipMemsetAsync(c->memo, 0, c->memo_alloc * 64, s), "memset memo table");
+    if (((++c->memo_epoch) & 0xFFFFFFu) == 0u) {   // 24-bit tags wrapped: clear
+        HIP_TRY(c, hipMemsetAsync(c->memo, 0, c->memo_alloc * 64, s), "memset memo table");
+        ++c->memo_epoch;
+    }
     *out = c->memo;
+    *epoch = c->memo_epoch;
     return QSMD_OK;
 }
 
@@ -570,6 +592,10 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         wp.explore_cap_wide = split ? 16 * c->split_budget : 0;   // (the giant stage's whole-search cap)
         wp.stats = c->wave_stats;
         wp.memo_min_rem = (uint32_t)c->wave_min_rem;
+        wp.dag_states = (uint32_t)(c->dag_states & ~1ull);   // (even: the DAG's LDS arrays stay 8-B aligned)
+        wp.dag_items = 4u * wp.dag_states;
+        wp.dbg = c->dag_dbg;
+        wp.dbg_h = (uint32_t)c->dag_dbg_h;
         wp.memo_mode = (flags & QSMD_FLAG_MEMO) ? 1u : 0u;
         // LDS memo table: 8 KB per wavefront (256 entries of <= 64 events),
         // 64 KB when the last call had wide histories (1024 entries of <= 128)
@@ -608,7 +634,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     p.probe_host = c->probe_host;
     p.stall_ticks = c->giant_stall_us * 100ull;   // 100 MHz s_memrealtime
     if (flags & QSMD_FLAG_MEMO) {
-        rc = memo_prepare(c, s, &p.memo);
+        rc = memo_prepare(c, s, &p.memo, &p.memo_epoch);
         if (rc) return rc;
         p.memo_mask = c->memo_alloc - 1;
     } else if (c->split_xmemo) {        // exact-count memo for the giants (the reference's counts)
@@ -677,6 +703,24 @@ int qsmd_check_batch_device(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr_
                                max_nodes, status_dev, nodes_dev, witness_dev, totals_dev, s);
 }
 
+// Grow the pinned host mirror of the io buffer (the previous call is done
+// with it: the host entry point synchronises before it returns).
+static int grow_pinned(qsmd_ctx* c, size_t need) {
+    if (c->pin_bytes >= need) return QSMD_OK;
+    quiesce(c);
+    if (c->pin) (void)hipHostFree(c->pin);
+    c->pin = nullptr;
+    c->pin_bytes = 0;
+    const size_t sz = std::max(need, (size_t)64 * 1024);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&c->pin), sz, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(c, QSMD_ERR_NOMEM, "hipHostMalloc", e);
+    }
+    c->pin_bytes = sz;
+    return QSMD_OK;
+}
+
 int qsmd_check_batch(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, uint64_t n_hist,
                      const qsmd_event* events, uint64_t n_events, const void* model0, uint32_t flags,
                      uint64_t max_nodes, uint8_t* status_out, uint64_t* nodes_out, uint8_t* witness_out,
@@ -689,35 +733,38 @@ int qsmd_check_batch(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, uint64
     hipStream_t s = c->stream;
     if (c->in_flight && c->last_stream != s) HIP_TRY(c, hipStreamWaitEvent(s, c->done_ev, 0), "hipStreamWaitEvent");
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness_out;
+    // io layout: [hdr | events | witness] copied in, [witness | status | nodes | totals] copied out
     const size_t o_hdr = 0;
-    const size_t o_ev = o_hdr + align_up(n_hist * sizeof(qsmd_hdr));
-    const size_t o_st = o_ev + align_up(n_events * sizeof(qsmd_event));
-    const size_t o_nd = o_st + align_up(n_hist);
-    const size_t o_w = o_nd + align_up(n_hist * 8);
-    const size_t o_tot = o_w + align_up(want_w ? n_events : 0);
-    const size_t need = o_tot + align_up(sizeof(qsmd_totals));
+    const size_t o_ev = o_hdr + align_up(n_hist * sizeof(qsmd_hdr), 16);
+    const size_t o_w = o_ev + align_up(n_events * sizeof(qsmd_event), 16);
+    const size_t o_st = o_w + align_up(want_w ? n_events : 0, 16);
+    const size_t o_nd = o_st + align_up(n_hist, 16);
+    const size_t o_tot = o_nd + align_up(n_hist * 8, 16);
+    const size_t need = o_tot + align_up(sizeof(qsmd_totals), 16);
     int rc = grow(c, &c->io, &c->io_bytes, need);
     if (rc) return rc;
+    rc = grow_pinned(c, need);
+    if (rc) return rc;
+    if (n_hist) std::memcpy(c->pin + o_hdr, hdr, n_hist * sizeof(qsmd_hdr));
+    if (n_events) std::memcpy(c->pin + o_ev, events, n_events * sizeof(qsmd_event));
+    if (want_w) std::memset(c->pin + o_w, 0xFF, n_events);
     auto* d_hdr = reinterpret_cast<qsmd_hdr*>(c->io + o_hdr);
     auto* d_ev = reinterpret_cast<qsmd_event*>(c->io + o_ev);
     auto* d_st = reinterpret_cast<uint8_t*>(c->io + o_st);
     auto* d_nd = reinterpret_cast<uint64_t*>(c->io + o_nd);
     auto* d_w = reinterpret_cast<uint8_t*>(c->io + o_w);
     auto* d_tot = reinterpret_cast<qsmd_totals*>(c->io + o_tot);
-    if (n_hist) HIP_TRY(c, hipMemcpyAsync(d_hdr, hdr, n_hist * sizeof(qsmd_hdr), hipMemcpyHostToDevice, s), "H2D hdr");
-    if (n_events) HIP_TRY(c, hipMemcpyAsync(d_ev, events, n_events * sizeof(qsmd_event), hipMemcpyHostToDevice, s), "H2D events");
-    if (want_w) HIP_TRY(c, hipMemsetAsync(d_w, 0xFF, n_events, s), "memset witness");
+    if (o_st) HIP_TRY(c, hipMemcpyAsync(c->io, c->pin, o_st, hipMemcpyHostToDevice, s), "H2D inputs");
     rc = check_device_locked(c, model_id, d_hdr, n_hist, d_ev, n_events, model0, flags, max_nodes, d_st, d_nd,
                              want_w ? d_w : nullptr, d_tot, s);
     if (rc) return rc;
-    if (n_hist) HIP_TRY(c, hipMemcpyAsync(status_out, d_st, n_hist, hipMemcpyDeviceToHost, s), "D2H status");
-    if (n_hist && nodes_out) HIP_TRY(c, hipMemcpyAsync(nodes_out, d_nd, n_hist * 8, hipMemcpyDeviceToHost, s), "D2H nodes");
-    if (want_w) HIP_TRY(c, hipMemcpyAsync(witness_out, d_w, n_events, hipMemcpyDeviceToHost, s), "D2H witness");
-    qsmd_totals t{};
-    HIP_TRY(c, hipMemcpyAsync(&t, d_tot, sizeof t, hipMemcpyDeviceToHost, s), "D2H totals");
+    HIP_TRY(c, hipMemcpyAsync(c->pin + o_w, c->io + o_w, need - o_w, hipMemcpyDeviceToHost, s), "D2H outputs");
     HIP_TRY(c, hipStreamSynchronize(s), "hipStreamSynchronize");
     c->in_flight = false;
-    if (totals_out) *totals_out = t;
+    if (n_hist) std::memcpy(status_out, c->pin + o_st, n_hist);
+    if (n_hist && nodes_out) std::memcpy(nodes_out, c->pin + o_nd, n_hist * 8);
+    if (want_w) std::memcpy(witness_out, c->pin + o_w, n_events);
+    if (totals_out) std::memcpy(totals_out, c->pin + o_tot, sizeof(qsmd_totals));
     return QSMD_OK;
 }
 
@@ -1007,7 +1054,7 @@ int qsmd_check_tasks(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, const 
     p.task_witness = want_w ? reinterpret_cast<uint8_t*>(c->sx + o_tw) : nullptr;
     p.external_tasks = 1;
     if (flags & QSMD_FLAG_MEMO) {
-        rc = memo_prepare(c, s, &p.memo);
+        rc = memo_prepare(c, s, &p.memo, &p.memo_epoch);
         if (rc) return rc;
         p.memo_mask = c->memo_alloc - 1;
     }

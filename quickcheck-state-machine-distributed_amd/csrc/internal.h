@@ -159,7 +159,7 @@ struct SplitArgs {
     unsigned long long* memo;     // QSMD_FLAG_MEMO table (8 x u64 per entry), the exact memo's, or null
     uint64_t memo_mask;           // entries - 1
     uint32_t memo_exact;          // 1: exact-count memo (16 x u64 per entry, epoch-tagged)
-    uint32_t memo_epoch;          // exact memo: this call's tag (24 bits)
+    uint32_t memo_epoch;          // this call's tag in either table (24 bits)
     uint32_t external_tasks;      // tasks given by the caller (qsmd_check_tasks)
     uint32_t early;               // QSMD_FLAG_EARLY_EXIT_BATCH: the fixup phase runs
     qsmd_totals* totals;          // the call's totals (device), written by the last block
@@ -228,7 +228,12 @@ struct WaveArgs {
     uint32_t memo_mode;           // QSMD_FLAG_MEMO: a memo hit counts nothing (explored nodes)
     uint32_t buckets;             // LDS memo table: buckets of 64 words (a power of two)
     uint32_t wide128;             // a second launch searches the wide list's 65..128-event histories
-    unsigned long long* stats;    // diagnostic: DFS iterations [max, sum], s_memtime cycles [max, sum], nodes sum
+    uint32_t dag_states;          // state-DAG capacity per wavefront (0 = DFS only; <= 4095)
+    uint32_t dag_items;           // its capacity in (state, candidate) items (<= 65535)
+    uint32_t* dbg;                // diagnostic (dag_debug_ptr): the DAG arrays of history dbg_h, or null
+    uint32_t dbg_h;
+    unsigned long long* stats;    // diagnostic: DFS iterations [max, sum], s_memtime cycles [max, sum], nodes sum,
+                                  // DAG-searched histories, their s_memtime cycles max
 };
 hipError_t launch_wave(const WaveArgs& p, uint32_t grid, uint32_t grid128, hipStream_t s);
 

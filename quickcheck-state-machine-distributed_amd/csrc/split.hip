@@ -150,12 +150,18 @@ struct Memo {
         }
     }
 
+    // ---- QSMD_FLAG_MEMO table: 8 x u64 per entry = [tag | key 7]; tag =
+    // epoch24 << 40 | k.tag (the giant | hash7), the same claim / ready
+    // protocol; entries of an older call (epoch) count as empty, so the table
+    // is cleared only when allocated (and when the 24-bit epochs wrap)
+    __device__ uint64_t mtag(const MemoKey& k) const { return ((uint64_t)(epoch & 0xFFFFFFu) << 40) | k.tag; }
     __device__ bool lookup(const MemoKey& k) const {
+        const uint64_t want = mtag(k);
         for (int i = 0; i < kMemoProbe; ++i) {
             const unsigned long long* e = tab + ((k.hash + (uint64_t)i) & mask) * 8u;
             const uint64_t t = ld_sc1(e);
-            if (t == 0) return false;
-            if ((t | 1ull) != (k.tag | 1ull) || !(t & 1ull)) continue;
+            if (t == 0 || stale(t)) return false;
+            if ((t | 1ull) != (want | 1ull) || !(t & 1ull)) continue;
             bool eq = true;
 #pragma unroll
             for (int q = 0; q < kMemoKey; ++q) eq = eq & (ld_sc1(e + 1 + q) == k.w[q]);
@@ -165,20 +171,22 @@ struct Memo {
     }
 
     __device__ void insert(const MemoKey& k) const {
+        const uint64_t want = mtag(k);
         for (int i = 0; i < kMemoProbe; ++i) {
             unsigned long long* e = tab + ((k.hash + (uint64_t)i) & mask) * 8u;
             uint64_t t = ld_sc1(e);
-            if (t == 0) {
-                t = atomicCAS(e, 0ull, (unsigned long long)k.tag);
-                if (t == 0) {
+            while (t == 0 || stale(t)) {
+                const uint64_t old = atomicCAS(e, (unsigned long long)t, (unsigned long long)want);
+                if (old == t) {
 #pragma unroll
                     for (int q = 0; q < kMemoKey; ++q) st_sc1(e + 1 + q, k.w[q]);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __hip_atomic_fetch_or(e, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     return;
                 }
+                t = old;
             }
-            if ((t | 1ull) == (k.tag | 1ull)) {
+            if ((t | 1ull) == (want | 1ull)) {
                 if (!(t & 1ull)) return;          // being written (likely this very key)
                 bool eq = true;
 #pragma unroll
@@ -384,7 +392,7 @@ struct GenDFS {
 #pragma unroll
         for (int q = 0; q < kMemoKey; ++q) h = mix64(h ^ k.w[q]);
         k.hash = h;
-        k.tag = ((uint64_t)(id + 1u) << 32) | ((h >> 32) & 0xFFFFFFFEull);
+        k.tag = ((uint64_t)(id + 1u) << 8) | ((h >> 56) & 0xFEull);   // (id + 1 < 2^32: below the epoch)
         return k;
     }
 

@@ -81,6 +81,11 @@ template <> __device__ __forceinline__ M128 mbit<M128>(uint32_t j) {
     return mk128(j < 64u ? 1ull << (j & 63u) : 0ull, j < 64u ? 0ull : 1ull << (j & 63u));
 }
 __device__ __forceinline__ uint64_t mlowest(uint64_t m) { return m & (0ull - m); }
+// per-lane select, word by word (a select of whole M128 objects goes through scratch)
+__device__ __forceinline__ uint64_t msel(bool c, uint64_t a, uint64_t b) { return c ? a : b; }
+__device__ __forceinline__ M128 msel(bool c, const M128& a, const M128& b) {
+    return mk128(c ? a.lo : b.lo, c ? a.hi : b.hi);
+}
 __device__ __forceinline__ M128 mlowest(const M128& m) { return MaskOps<M128>::lowest(m); }
 // the bits above j
 __device__ __forceinline__ uint64_t mabove(uint32_t j, uint64_t) { return ~1ull << j; }
@@ -338,12 +343,461 @@ __device__ __forceinline__ void wave_insert(uint32_t* tab, const WKey& k, uint32
         tab[k.bucket * 64u + (uint32_t)lane] = ((uint32_t)lane % EW) == 3u ? count : k.vec;
 }
 
+// ---------------------------------------------------------------- state DAG
+// The subtree below a node is a function of its state S = (remaining events,
+// model) (Lemma L1), so the reference's search tree folds into a DAG of
+// states: level d holds the states after d operations (popcount(rem) = n_ev -
+// 2d, so an edge always goes one level down and equal states meet only within
+// a level).  The wavefront builds it level by level -- a level's states in
+// lanes, then its (state, candidate) items in lanes: findResponse, filter1,
+// postcondition, transition; the children deduplicated by full-key compare --
+// and folds it back from the deepest level:
+//   g(S) = over S's children in candidate order: +1 node each (the step
+//          call); a raising postcondition decides (MODEL_ERROR); a True one
+//          adds the child's count and decides when g(child) does (True or
+//          raise); no child at all: True (any' []), or False at the root (any).
+// That is exactly the DFS's accumulation (src/Linearisability.hs:59-69): the
+// node count, verdict and -- by following the deciding child from the root --
+// the witness are the reference's, with every state evaluated once.  With
+// QSMD_FLAG_MEMO the count is the explored-node count of the DFS that prunes
+// known-failing states (oracle/ref_cpu.c): the decision path's evaluated
+// children plus, once each, every state below a failed earlier sibling.
+// Histories whose DAG does not fit (a level wider than 64 states or items,
+// more than the capacity in states or items) run the DFS below instead.
+enum : uint32_t { G_F = 0u, G_T = 1u, G_ERR = 2u, G_SAT = 4u, G_MARK = 8u };
+
+template <typename M> struct DagGeo;
+template <> struct DagGeo<uint64_t> { static constexpr uint32_t NM = 2; };
+template <> struct DagGeo<M128> { static constexpr uint32_t NM = 4; };
+
+__device__ __forceinline__ void mwords(uint64_t m, uint32_t* w) {
+    w[0] = (uint32_t)m;
+    w[1] = (uint32_t)(m >> 32);
+}
+__device__ __forceinline__ void mwords(const M128& m, uint32_t* w) {
+    w[0] = (uint32_t)m.lo;
+    w[1] = (uint32_t)(m.lo >> 32);
+    w[2] = (uint32_t)m.hi;
+    w[3] = (uint32_t)(m.hi >> 32);
+}
+template <typename M> __device__ __forceinline__ M mfrom(const uint32_t* w);
+template <> __device__ __forceinline__ uint64_t mfrom<uint64_t>(const uint32_t* w) {
+    return w[0] | (uint64_t)w[1] << 32;
+}
+template <> __device__ __forceinline__ M128 mfrom<M128>(const uint32_t* w) {
+    return mk128(w[0] | (uint64_t)w[1] << 32, w[2] | (uint64_t)w[3] << 32);
+}
+
+// The wavefront's DAG arrays in LDS (the keys stay in lanes).
+constexpr uint32_t kDagSlots = 1024;   // dedup table: a level's children by key hash
+struct DagLds {
+    uint32_t* sitem;   // [SC]: first item | item count << 16
+    uint32_t* glo;     // [SC]: g count, low / high word
+    uint32_t* ghi;
+    uint32_t* gfl;     // [SC]: g result | G_SAT | G_MARK
+    uint32_t* item;    // [IC]: child | post << 12 | j << 14 (child 0xFFF: none)
+    uint32_t* evlo;    // [128]: event lo words
+    int32_t* evval;    // [128]: event values
+    uint32_t* tab;     // [kDagSlots]: lowest lane holding a child of that hash slot (~0u: none)
+    uint32_t* path;    // [128]: the deciding path's candidate per depth
+};
+
+template <uint32_t MODEL, typename M>
+struct DagKey {
+    static constexpr uint32_t NM = DagGeo<M>::NM;
+    static constexpr uint32_t MWD = MODEL == QSMD_MODEL_BANK ? 9u : 2u;
+    static constexpr uint32_t KW = NM + MWD;   // key words: rem, then the model (Bank: ex, 8 balances; Ticket: just, n)
+};
+
+template <uint32_t MODEL, typename M>
+__host__ __device__ constexpr size_t dag_lds_bytes(uint32_t SC, uint32_t IC) {
+    return (size_t)SC * 16u + (size_t)IC * 4u + 128u * 8u + kDagSlots * 4u + 128u * 4u;
+}
+
+template <uint32_t MODEL, typename M>
+__device__ __forceinline__ DagLds dag_carve(uint32_t* base, uint32_t SC, uint32_t IC) {
+    DagLds L;
+    L.sitem = base;
+    L.glo = L.sitem + SC;
+    L.ghi = L.glo + SC;
+    L.gfl = L.ghi + SC;
+    L.item = L.gfl + SC;
+    L.evlo = L.item + IC;
+    L.evval = reinterpret_cast<int32_t*>(L.evlo + 128);
+    L.tab = reinterpret_cast<uint32_t*>(L.evval + 128);
+    L.path = L.tab + kDagSlots;
+    return L;
+}
+
+
+// A key's 32-bit hash: independent products folded together (a short chain)
+template <uint32_t KW>
+__device__ __forceinline__ uint32_t dag_hash(const uint32_t* kw) {
+    constexpr uint32_t C[4] = {0x9E3779B1u, 0x85EBCA77u, 0xC2B2AE3Du, 0x27D4EB2Fu};
+    uint32_t h[4] = {0x165667B1u, 0xD3A2646Cu, 0xFD7046C5u, 0xB55A4F09u};
+#pragma unroll
+    for (uint32_t k = 0; k < KW; ++k) h[k & 3u] ^= __builtin_rotateleft32(kw[k] * C[k & 3u], 5u * k);
+    uint32_t x = (h[0] ^ h[1]) + (h[2] ^ h[3]);
+    x ^= x >> 16;
+    x *= 0x7FEB352Du;
+    x ^= x >> 15;
+    return x;
+}
+
+// The DAG search of the staged history (d: events in lanes, INV / RESP);
+// QSMD_STATUS_* or -1 when the DAG does not fit.  Witness path in L.path.
+template <uint32_t MODEL, typename M>
+__device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS<MODEL, M>& d, uint32_t n_ev,
+                           uint32_t n_pid, const DagLds& L, uint32_t SC, uint32_t IC, int lane, uint64_t& nodes_out,
+                           uint32_t& path_len) {
+    using K = DagKey<MODEL, M>;
+    constexpr uint32_t NM = K::NM, KW = K::KW;
+    constexpr bool BANK = MODEL == QSMD_MODEL_BANK;
+    const uint32_t ul = (uint32_t)lane;
+    // events into LDS, the per-pid invocation / response masks (scalars)
+#pragma unroll
+    for (uint32_t w = 0; w < Geo<M>::NW; ++w) {
+        const uint32_t e = ul + 64u * w;
+        if (e < n_ev) {
+            L.evlo[e] = d.lo[w];
+            L.evval[e] = d.val[w];
+        }
+    }
+    for (uint32_t i = ul; i < kDagSlots; i += 64u) L.tab[i] = ~0u;
+    // the events of pid q: one lane compare per event register (a ballot,
+    // recomputed where needed: the masks of 8 pids would not stay in SGPRs;
+    // called in uniform control flow only, every lane active)
+    auto pid_ev = [&](uint32_t q) -> M {
+        if constexpr (Geo<M>::NW == 1) return __ballot(d.pidv[0] == q);
+        else return mk128(__ballot(d.pidv[0] == q), __ballot(d.pidv[1] == q));
+    };
+    // ---- forward: the levels.  A level's states live in lanes (SM: which
+    // ones; kw: the key, sid: the state id); its items (one per candidate
+    // with a response, in candidate order per state) in lanes 0..total-1;
+    // the leaders of the children's dedup become the next level's state lanes
+    uint32_t kw[KW];
+    mwords(d.INV | d.RESP, kw);
+    if constexpr (BANK) {
+        kw[NM] = a.m0_exists;
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) kw[NM + 1 + q] = (uint32_t)(int32_t)a.m0_val[q];
+    } else {
+        kw[NM] = a.m0_just;
+        kw[NM + 1] = (uint32_t)(int32_t)a.m0_val[0];
+    }
+    // level boundaries in lanes: lane d of lv0 (d < 64) / lv1 (64 + d) = the first state of level d
+    uint32_t lv0 = ul == 1u ? 1u : 0u, lv1 = 0u;
+    uint64_t SM = 1ull;                                     // the root, in lane 0
+    uint32_t sid = 0u;
+    uint32_t n_states = 1u, n_items = 0u, nlev = 1u;
+    bool fit = true;
+    const bool timing = p.stats != nullptr;
+    uint64_t tph[5] = {0, 0, 0, 0, 0}, tprev = timing ? __builtin_amdgcn_s_memtime() : 0ull;
+    auto tick = [&](int k) {
+        if (timing) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            tph[k] += t - tprev;
+            tprev = t;
+        }
+    };
+    while (true) {
+        // state lanes: the candidates with a response (takeInvocations, findResponse)
+        const bool sl = (SM >> ul) & 1ull;
+        const M rem = mfrom<M>(kw);
+        const M C = mcands(rem, d.INV, d.RESP);
+        M V{};
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {              // (the ballots in uniform control flow)
+            if (q >= n_pid) break;
+            const M pq = pid_ev(q);
+            V = msel(mnz(rem & pq & d.RESP), V | (C & pq), V);
+        }
+        V = msel(sl, V, M{});
+        const uint32_t deg = mpop(V);
+        // the items' offsets: a prefix sum of deg over the lanes, from ballots of its bits
+        uint32_t excl = 0u, total = 0u;
+        for (uint32_t b = 0; b < 8; ++b) {
+            const uint64_t bm = __ballot((deg >> b) != 0u);
+            if (!bm) break;
+            const uint64_t bb = __ballot((deg >> b) & 1u);
+            excl += lane_prefix(bb) << b;
+            total += (uint32_t)__builtin_popcountll(bb) << b;
+        }
+        if (total > 64u || n_items + total > IC) { fit = false; break; }
+        if (sl) L.sitem[sid] = (n_items + excl) | deg << 16;
+        tick(0);
+        if (total == 0u) break;                             // every state of the level is a leaf
+        // item lane i: its state lane (the last with items at or below i), the
+        // t-th candidate of that state
+        const bool il = ul < total;
+        uint32_t src = 0u, e0 = 0u;
+        for (uint64_t m = SM & __ballot(deg != 0u); m; m &= m - 1ull) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(m);
+            const uint32_t e = rl(excl, l);
+            src = ul >= e ? l : src;
+            e0 = ul >= e ? e : e0;
+        }
+        uint32_t skw[KW], vw[NM];
+#pragma unroll
+        for (uint32_t k = 0; k < KW; ++k) skw[k] = (uint32_t)__shfl((int)kw[k], (int)src, 64);
+        {
+            uint32_t vv[NM];
+            mwords(V, vv);
+#pragma unroll
+            for (uint32_t k = 0; k < NM; ++k) vw[k] = (uint32_t)__shfl((int)vv[k], (int)src, 64);
+        }
+        M Vs = mfrom<M>(vw);
+        for (uint32_t t = il ? ul - e0 : 0u; t; --t) Vs &= ~mlowest(Vs);
+        const uint32_t j = il ? mctz(Vs) : 0u;
+        // its pid's masks: response r (findResponse) and first invocation fi (filter1)
+        M Pj = pid_ev(0);
+        const M jb = mbit<M>(j);
+#pragma unroll
+        for (uint32_t q = 1; q < 8; ++q) {
+            if (q >= n_pid) break;
+            const M pq = pid_ev(q);
+            Pj = msel(mnz(pq & jb), pq, Pj);
+        }
+        const M PIj = Pj & d.INV, PRj = Pj & d.RESP;
+        const M rems = mfrom<M>(skw);
+        const M rr = rems & PRj;
+        const uint32_t r = mnz(rr) ? mctz(rr) : j, fi = mctz(rems & PIj);
+        const uint32_t lj = L.evlo[j], lr = L.evlo[r];
+        const int32_t m = L.evval[j], rv = L.evval[r];
+        const uint32_t code = (lj >> 8) & 0xFFu, rc = (lr >> 8) & 0xFFu;
+        uint32_t res;
+        if constexpr (BANK) {
+            const uint32_t ex = skw[NM];
+            const uint32_t ia = (lj >> 16) & 7u, ib = (lj >> 24) & 7u;
+            int32_t bal_a = 0, bal_b = 0;
+            bool neg = false;
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) {
+                const int32_t bq = (int32_t)skw[NM + 1 + q];
+                bal_a = q == ia ? bq : bal_a;
+                bal_b = q == ib ? bq : bal_b;
+                neg = neg || (((ex >> q) & 1u) && bq < 0);
+            }
+            const uint32_t ex_a = (ex >> ia) & 1u, ex_b = (ex >> ib) & 1u;
+            // post (test/Bank.hs:118-131): the invariant, then the expected response
+            const bool tr = code == QSMD_BANK_TRANSFER, chk = code == QSMD_BANK_CHECK_BALANCE;
+            const bool same = ia == ib;
+            const uint32_t sel = (code == QSMD_BANK_OPEN_ACCOUNT || bal_a >= m) ? ex_a : 0u;
+            const uint32_t exp = (kBankExp2 >> (code * 6u + sel * 3u)) & 7u;
+            const bool err = !neg && chk && rc == QSMD_BANK_BALANCE && !ex_a;   // Map.! raises
+            const bool ok = !neg && !err && rc == exp && (!chk || rv == bal_a);
+            res = err ? G_ERR : (ok ? G_T : G_F);
+            // next' (test/Bank.hs:92-101)
+            const int32_t sa = bank_sign(code);
+            const int32_t na = (ex_a ? bal_a : 0) + (ex_a ? sa : (sa & 1)) * m;
+            const int32_t bo = same ? na : bal_b;
+            const int32_t fb = tr ? (((ex_b != 0u) || same) ? bo : 0) + m : bo;
+            skw[NM] = ex | ((chk ? 0u : 1u) << ia) | ((tr ? 1u : 0u) << ib);
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) {
+                uint32_t v = skw[NM + 1 + q];
+                v = q == ia ? (uint32_t)na : v;
+                v = (tr && q == ib) ? (uint32_t)fb : v;
+                skw[NM + 1 + q] = v;
+            }
+        } else {
+            // TicketDispenser (test/TicketDispenser.hs:81-102)
+            const uint32_t just = skw[NM];
+            const int32_t tn = (int32_t)skw[NM + 1];
+            const bool tt = code == QSMD_TICKET_TAKE_TICKET;
+            const bool ok = tt ? (rc == QSMD_TICKET_NUMBER && just != 0u && rv == tn + 1) : rc == QSMD_TICKET_OK;
+            res = ok ? G_T : G_F;
+            skw[NM] = 1u;
+            skw[NM + 1] = tt ? (uint32_t)(tn + 1) : 0u;
+        }
+        {   // the child's remaining events: the pid's first invocation and its response gone
+            uint32_t w2[NM];
+            mwords(rems & ~(mbit<M>(fi) | mbit<M>(r)), w2);
+#pragma unroll
+            for (uint32_t k = 0; k < NM; ++k) skw[k] = w2[k];
+        }
+        tick(1);
+        // children: one state per distinct key.  Lanes meet in a hash slot;
+        // its lowest lane leads when the full keys agree; the rest (a slot
+        // shared by different keys) go through a leader loop
+        const bool isT = il && res == G_T;
+        uint32_t child = 0xFFFu;
+        uint64_t LM = 0ull;
+        uint64_t pending = __ballot(isT);
+        if (__builtin_popcountll(pending) > 2) {
+            const uint32_t slot = dag_hash<KW>(skw) >> 22;
+            if (isT) atomicMin(&L.tab[slot], ul);
+            __syncthreads();
+            const uint32_t w = isT ? L.tab[slot] : ul;
+            bool eq = true;
+#pragma unroll
+            for (uint32_t k = 0; k < KW; ++k) eq = eq && skw[k] == (uint32_t)__shfl((int)skw[k], (int)w, 64);
+            const bool lead = isT && w == ul;
+            LM = __ballot(lead);
+            if (isT && eq) child = n_states + (uint32_t)__builtin_popcountll(LM & ((1ull << w) - 1ull));
+            n_states += (uint32_t)__builtin_popcountll(LM);
+            if (isT) L.tab[slot] = ~0u;                     // (every lane of the slot has read it)
+            pending = __ballot(isT && !eq);
+        }
+        while (pending) {
+            const uint32_t ldr = (uint32_t)__builtin_ctzll(pending);
+            bool e2 = true;
+#pragma unroll
+            for (uint32_t k = 0; k < KW; ++k) e2 = e2 && skw[k] == rl(skw[k], ldr);
+            const uint64_t same = __ballot(e2) & pending;
+            child = (same >> ul) & 1ull ? n_states : child;
+            ++n_states;
+            LM |= 1ull << ldr;
+            pending &= ~same;
+        }
+        if (n_states > SC) { fit = false; break; }
+        if (il) L.item[n_items + ul] = child | res << 12 | j << 14;
+        n_items += total;
+        lv0 = ul == nlev + 1u ? n_states : lv0;
+        lv1 = ul + 64u == nlev + 1u ? n_states : lv1;
+        // the next level: the leaders, with their children's keys
+        SM = LM;
+        sid = child;
+#pragma unroll
+        for (uint32_t k = 0; k < KW; ++k) kw[k] = skw[k];
+        tick(2);
+        if (!LM) break;                                     // no new state: the last level
+        ++nlev;
+    }
+    __syncthreads();
+    if (!fit) return -1;
+
+    auto lvl_at = [&](uint32_t k) { return k < 64u ? rl(lv0, k) : rl(lv1, k - 64u); };
+    // ---- backward: g of every state, deepest level first (a state's items
+    // and their children's g read 4 at a time, then folded in order)
+    for (int lv = (int)nlev - 1; lv >= 0; --lv) {
+        const uint32_t b0 = lvl_at((uint32_t)lv), b1 = lvl_at((uint32_t)lv + 1u);
+        const uint32_t s = b0 + ul;
+        if (s < b1) {
+            const uint32_t xi = L.sitem[s];
+            const uint32_t off = xi & 0xFFFFu, deg = xi >> 16;
+            uint64_t c = 0ull;
+            uint32_t res = deg ? G_F : (s ? G_T : G_F), sat = 0u;
+            bool done = false;
+            for (uint32_t base = 0; base < deg && !done; base += 4u) {
+                uint32_t it[4], cl[4], chh[4], cf[4];
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t) it[t] = base + t < deg ? L.item[off + base + t] : 0u;
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t) {
+                    const bool tc = ((it[t] >> 12) & 3u) == G_T && base + t < deg;
+                    const uint32_t ch = tc ? it[t] & 0xFFFu : 0u;
+                    cl[t] = tc ? L.glo[ch] : 0u;
+                    chh[t] = tc ? L.ghi[ch] : 0u;
+                    cf[t] = tc ? L.gfl[ch] : G_F;
+                }
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t) {
+                    if (done || base + t >= deg) continue;
+                    const uint32_t post = (it[t] >> 12) & 3u;
+                    c += 1ull;
+                    if (post == G_ERR) {
+                        res = G_ERR;
+                        done = true;
+                    } else if (post == G_T) {
+                        uint64_t sum;
+                        sat |= (cf[t] & G_SAT) |
+                               (__builtin_add_overflow(c, cl[t] | (uint64_t)chh[t] << 32, &sum) ? G_SAT : 0u);
+                        c = sum;
+                        if ((cf[t] & 3u) != G_F) {
+                            res = cf[t] & 3u;
+                            done = true;
+                        }
+                    }
+                }
+            }
+            L.glo[s] = (uint32_t)c;
+            L.ghi[s] = (uint32_t)(c >> 32);
+            L.gfl[s] = res | sat;
+        }
+        __syncthreads();
+    }
+    tick(3);
+    const uint32_t f0 = L.gfl[0];
+    const uint32_t res0 = f0 & 3u;
+    const bool memo = p.memo_mode != 0u;
+    // ---- the deciding path (the witness; QSMD_FLAG_MEMO: its evaluated
+    // children, and the failed earlier siblings marked)
+    uint64_t mcount = 0ull;
+    path_len = 0u;
+    if (res0 == G_T || memo) {
+        uint32_t s = 0u;
+        while (true) {
+            const uint32_t xi = L.sitem[s];
+            const uint32_t off = xi & 0xFFFFu, deg = xi >> 16;
+            if (deg == 0u) break;
+            uint32_t it = 0u, post = G_F, ch = 0u, cf = G_F;
+            if (ul < deg) {
+                it = L.item[off + ul];
+                post = (it >> 12) & 3u;
+                ch = post == G_T ? it & 0xFFFu : 0u;
+                cf = post == G_T ? (L.gfl[ch] & 3u) : G_F;
+            }
+            const uint64_t dec = __ballot(ul < deg && (post == G_ERR || cf != G_F));
+            const uint32_t k = dec ? (uint32_t)__builtin_ctzll(dec) : deg;
+            mcount += dec ? k + 1u : deg;
+            if (memo && ul < k && post == G_T) L.gfl[ch] = L.gfl[ch] | G_MARK;
+            if (!dec) break;
+            const uint32_t itk = rl(it, k);
+            if (((itk >> 12) & 3u) == G_ERR) break;
+            if (ul == 0) L.path[path_len] = (itk >> 14) & 127u;
+            ++path_len;
+            s = itk & 0xFFFu;
+        }
+        __syncthreads();
+    }
+    if (memo) {
+        // the marked states' subtrees, level by level: each state counted once
+        uint64_t part = 0ull;
+        for (uint32_t lv = 1; lv < nlev; ++lv) {
+            const uint32_t b0 = lvl_at(lv), b1 = lvl_at(lv + 1u);
+            const uint32_t s = b0 + ul;
+            if (s < b1 && (L.gfl[s] & G_MARK)) {
+                const uint32_t xi = L.sitem[s];
+                const uint32_t off = xi & 0xFFFFu, deg = xi >> 16;
+                part += deg;
+                for (uint32_t t = 0; t < deg; ++t) {
+                    const uint32_t it = L.item[off + t];
+                    if (((it >> 12) & 3u) == G_T) {
+                        const uint32_t ch = it & 0xFFFu;
+                        L.gfl[ch] = L.gfl[ch] | G_MARK;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        mcount += wave_sum64(part);
+    }
+    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
+    const uint64_t c0 = L.glo[0] | (uint64_t)L.ghi[0] << 32;
+    const uint64_t n = memo ? mcount : c0;
+    __syncthreads();
+    tick(4);
+    if (timing && ul == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) atomicAdd(p.stats + 8 + k, (unsigned long long)tph[k]);
+        atomicAdd(p.stats + 13, (unsigned long long)nlev);
+    }
+    if ((!memo && (f0 & G_SAT)) || n > limit) {
+        nodes_out = limit;
+        return QSMD_STATUS_BUDGET;
+    }
+    nodes_out = n;
+    return res0 == G_T ? QSMD_STATUS_LINEARISABLE : (res0 == G_ERR ? QSMD_STATUS_MODEL_ERROR
+                                                                   : QSMD_STATUS_NONLINEARISABLE);
+}
+
 // One history h (its header H) searched by the whole wavefront (wide: from
 // stage 0w's deferred list).
 template <uint32_t MODEL, typename M>
 __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, const qsmd_hdr& H, bool wide,
                                              uint32_t* tab, uint32_t epoch, uint32_t& victim, int lane, uint64_t t0,
-                                             Counters& cnt) {
+                                             Counters& cnt, uint32_t* dag_base) {
     constexpr uint32_t NW = Geo<M>::NW, EW = Geo<M>::EW;
     const SearchArgs& a = p.s;
     const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
@@ -407,9 +861,47 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
     } else if (beyond_first_fail(a, h)) {
         status = QSMD_STATUS_SKIPPED;
     }
+    const uint64_t c0 = p.stats ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (status < 0 && dag_base) {                    // the state DAG, when it fits
+        const DagLds L = dag_carve<MODEL, M>(dag_base, p.dag_states, p.dag_items);
+        uint64_t dn = 0ull;
+        uint32_t plen = 0u;
+        const int ds = dag_history<MODEL, M>(p, a, d, n_ev, H.n_pid, L, p.dag_states, p.dag_items, lane, dn, plen);
+        if (ds >= 0) {
+            if (p.stats && lane == 0) {
+                const unsigned long long cyc = __builtin_amdgcn_s_memtime() - c0;
+                atomicAdd(p.stats + 5, 1ull);
+                atomicMax(p.stats + 6, cyc);
+                atomicAdd(p.stats + 7, cyc);
+            }
+            if (lane == 0) {
+                note_failure(a, h, ds);
+                a.status[h] = (uint8_t)ds;
+                if (a.nodes) a.nodes[h] = dn;
+                cnt.add(ds, dn);
+            }
+            if (p.dbg && h == p.dbg_h) {             // diagnostic: the DAG arrays of one history
+                const uint32_t* src = dag_base;
+                const uint32_t nw = (uint32_t)(dag_lds_bytes<MODEL, M>(p.dag_states, p.dag_items) / 4u);
+                for (uint32_t i = (uint32_t)lane; i < nw; i += 64u) p.dbg[16 + i] = src[i];
+                if (lane == 0) {
+                    p.dbg[0] = (uint32_t)ds;
+                    p.dbg[1] = (uint32_t)dn;
+                    p.dbg[2] = p.dag_states;
+                    p.dbg[3] = p.dag_items;
+                }
+            }
+            if (a.witness && ds == QSMD_STATUS_LINEARISABLE) {
+                uint8_t* w = a.witness + H.ev_off;
+                for (uint32_t k = (uint32_t)lane; k <= plen && k < n_ev; k += 64u)
+                    w[k] = k < plen ? (uint8_t)L.path[k] : QSMD_WITNESS_END;
+            }
+            __syncthreads();                         // (L.path read before the next history reuses it)
+            return;
+        }
+    }
     bool skip = false;
     uint32_t iter = 0;
-    const uint64_t c0 = p.stats ? __builtin_amdgcn_s_memtime() : 0ull;
     const uint32_t min_rem = p.memo_min_rem;
     const bool counts = !p.memo_mode;            // exact counts (else QSMD_FLAG_MEMO: explored nodes)
     const uint32_t cap = (uint32_t)min(wide ? p.explore_cap_wide : p.explore_cap, 0xFFFFFFFFull);
@@ -513,6 +1005,7 @@ __global__ __launch_bounds__(C_LANES) void wave_search(WaveArgs p) {
     const uint32_t n32 = W128 ? 0u : *p.count32, n64 = W128 ? 0u : *p.count64, nw = *p.count_wide;
     const uint64_t t0 = p.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     Counters cnt;
+    uint32_t* dag = p.dag_states ? tab + p.buckets * 64u : nullptr;
     clear_table(tab, p.buckets, lane);
     uint32_t epoch = 0u, victim = 0u;
     for (uint32_t i = blockIdx.x; i < n32 + n64 + nw; i += gridDim.x) {
@@ -532,24 +1025,41 @@ __global__ __launch_bounds__(C_LANES) void wave_search(WaveArgs p) {
             clear_table(tab, p.buckets, lane);
             epoch = 1u;
         }
-        wave_history<MODEL, M>(p, h, H, wide, tab, epoch, victim, lane, t0, cnt);
+        wave_history<MODEL, M>(p, h, H, wide, tab, epoch, victim, lane, t0, cnt, dag);
     }
     cnt.flush(p.s.buckets, lane);
 }
 
-hipError_t launch_wave(const WaveArgs& p, uint32_t grid, uint32_t grid128, hipStream_t s) {
-    const size_t lds = (size_t)p.buckets * 64u * 4u;
-    if (p.s.model_id == QSMD_MODEL_BANK)
-        hipLaunchKernelGGL((wave_search<QSMD_MODEL_BANK, uint64_t>), dim3(grid), dim3(C_LANES), lds, s, p);
-    else
-        hipLaunchKernelGGL((wave_search<QSMD_MODEL_TICKET, uint64_t>), dim3(grid), dim3(C_LANES), lds, s, p);
-    if (p.wide128) {
-        if (p.s.model_id == QSMD_MODEL_BANK)
-            hipLaunchKernelGGL((wave_search<QSMD_MODEL_BANK, M128>), dim3(grid128), dim3(C_LANES), lds, s, p);
-        else
-            hipLaunchKernelGGL((wave_search<QSMD_MODEL_TICKET, M128>), dim3(grid128), dim3(C_LANES), lds, s, p);
+// dynamic LDS of one workgroup: the memo table, then the DAG arrays
+template <uint32_t MODEL, typename M>
+static size_t wave_lds(const WaveArgs& p) {
+    return (size_t)p.buckets * 64u * 4u + (p.dag_states ? dag_lds_bytes<MODEL, M>(p.dag_states, p.dag_items) : 0u);
+}
+
+constexpr size_t kMaxLds = 160u * 1024u;   // gfx950: LDS per workgroup at most
+
+template <uint32_t MODEL, typename M>
+static hipError_t launch_one(WaveArgs p, uint32_t grid, hipStream_t s) {
+    while (p.dag_states && wave_lds<MODEL, M>(p) > kMaxLds) {   // a DAG capacity beyond the LDS: halved
+        p.dag_states = (p.dag_states / 2u) & ~1u;
+        p.dag_items = 4u * p.dag_states;
     }
+    const size_t lds = wave_lds<MODEL, M>(p);
+    if (lds > 64u * 1024u) {
+        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wave_search<MODEL, M>),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((wave_search<MODEL, M>), dim3(grid), dim3(C_LANES), lds, s, p);
     return hipGetLastError();
+}
+
+hipError_t launch_wave(const WaveArgs& p, uint32_t grid, uint32_t grid128, hipStream_t s) {
+    hipError_t e = p.s.model_id == QSMD_MODEL_BANK ? launch_one<QSMD_MODEL_BANK, uint64_t>(p, grid, s)
+                                                   : launch_one<QSMD_MODEL_TICKET, uint64_t>(p, grid, s);
+    if (e != hipSuccess || !p.wide128) return e;
+    return p.s.model_id == QSMD_MODEL_BANK ? launch_one<QSMD_MODEL_BANK, M128>(p, grid128, s)
+                                           : launch_one<QSMD_MODEL_TICKET, M128>(p, grid128, s);
 }
 
 }  // namespace qsmd

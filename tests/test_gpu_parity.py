@@ -97,7 +97,7 @@ def test_random_any_shape(ctx, model):
 
 DEFAULTS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
             "wave_grid": 0, "split_budget": 1024, "memo_lane_entries": 128, "memo_grid": 0, "split_xmemo": 1,
-            "memo_lds": 1}
+            "memo_lds": 1, "dag_states": 128}
 
 
 @pytest.fixture
@@ -199,15 +199,19 @@ def test_lane_mode(ctx, knobs, name, n, budget, max_nodes, entries, lds):
 
 
 @pytest.mark.parametrize("name,n,budget,max_nodes", LANE_CASES)
-@pytest.mark.parametrize("min_rem,grid", [(4, 0), (0, 0), (64, 0), (0, 7)])
-def test_wave_mode(ctx, knobs, name, n, budget, max_nodes, min_rem, grid):
+@pytest.mark.parametrize("min_rem,grid,dag", [(4, 0, 128), (4, 0, 0), (0, 0, 0), (64, 0, 0), (0, 7, 0),
+                                              (4, 7, 128), (4, 0, 6), (4, 0, 4095)])  # (4095: cut to the LDS)
+def test_wave_mode(ctx, knobs, name, n, budget, max_nodes, min_rem, grid, dag):
     """Wave mode of the heavy stage (csrc/wave.hip): one wavefront per
-    history, the DFS in wave-uniform registers, the exact-count memo in an
-    8-way LDS table per wavefront.  min_rem: memo only above this many
-    remaining events (64: no memo at all, 0: at every node); grid 7: few
-    wavefronts, many histories each (grid-stride, entry tags per history);
-    max_nodes falls inside reused subtrees."""
-    knobs(heavy_mode=0, wave_min_rem=min_rem, wave_grid=grid, stage0_budget=budget, stage0w_budget=budget)
+    history; the state DAG (dag: its capacity in states; 0 = off, 6 = most
+    histories overflow it mid-build and run the DFS) or the DFS in
+    wave-uniform registers with the exact-count memo in an 8-way LDS table
+    per wavefront.  min_rem: memo only above this many remaining events (64:
+    no memo at all, 0: at every node); grid 7: few wavefronts, many
+    histories each (grid-stride, entry tags per history); max_nodes falls
+    inside reused subtrees / below the DAG's exact count."""
+    knobs(heavy_mode=0, wave_min_rem=min_rem, wave_grid=grid, stage0_budget=budget, stage0w_budget=budget,
+          dag_states=dag)
     hdr, ev, _ = gen.generate_config(name, 6, n)
     _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
 
@@ -267,11 +271,11 @@ def test_tail_grids_follow_the_previous_call(ctx, knobs):
 
 
 @pytest.mark.parametrize("model", ["ticket", "bank"])
-@pytest.mark.parametrize("heavy", [0, 1])
-def test_heavy_any_shape(ctx, knobs, model, heavy):
+@pytest.mark.parametrize("heavy,dag", [(0, 128), (0, 0), (1, 128)])
+def test_heavy_any_shape(ctx, knobs, model, heavy, dag):
     """Unpaired, shared-pid, pending and stray-response histories (the
     general DFS mode), Map.! errors, node budgets and a non-default model0
-    through the heavy stage."""
+    through the heavy stage (wave mode: the state DAG, or the DFS)."""
     rng = random.Random(77 if model == "ticket" else 78)
     hs = []
     for _ in range(4000):
@@ -280,7 +284,7 @@ def test_heavy_any_shape(ctx, knobs, model, heavy):
         else:
             hs.append(histgen.wellformed_history(rng, model, rng.randint(6, 16), rng.randint(1, 5)))
     m = models.BY_NAME[model]
-    knobs(heavy_mode=heavy, stage0_budget=4, wave_min_rem=0)
+    knobs(heavy_mode=heavy, stage0_budget=4, wave_min_rem=0, dag_states=dag)
     b = codec.encode(m, hs)
     for max_nodes in (0, 50, 3000):
         _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=max_nodes)
