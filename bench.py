@@ -283,15 +283,24 @@ def extra_configs(dev, S, knobs):
     h, e, _ = gen.adversarial_ticket(8, 64, bug=True)
     ctx = device.Context(dev.index)
     times = []
-    for _ in range(4):
+    for _ in range(21):
         t = time.perf_counter()
         st, nd, _, _ = ctx.check_arrays(1, h, e, flags=device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_MEMO)
         times.append(time.perf_counter() - t)
     ctx.close()
     st_o, _, _ = oracle_c.check_batch(1, h, e, memo=True)
+    # the CPU point on this host: the C oracle's memo mode (the reference's
+    # search pruning known-failing states), one thread, the same history
+    cpu_t, cpu_n = time.perf_counter(), 0
+    while time.perf_counter() - cpu_t < 1.0:
+        oracle_c.check_batch(1, h, e, memo=True)
+        cpu_n += 1
+    cpu_ms = 1e3 * (time.perf_counter() - cpu_t) / cpu_n
     out["config4"] = {"workload": "adversarial TicketDispenser 8x64 (one history, QSMD_FLAG_MEMO, host entry)",
                       "ms_per_history": 1e3 * float(np.median(times[1:])), "verdict": int(st[0]),
-                      "verdict_matches_oracle": bool(int(st[0]) == int(st_o[0]))}
+                      "verdict_matches_oracle": bool(int(st[0]) == int(st_o[0])),
+                      "cpu_ms_per_history": cpu_ms,
+                      "cpu_sample": f"{cpu_n} calls of oracle/ref_cpu.c memo mode, 1 thread, through ctypes"}
     return out
 
 

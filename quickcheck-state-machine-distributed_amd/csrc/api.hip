@@ -42,6 +42,10 @@ struct qsmd_ctx {
     size_t io_bytes = 0;
     char* pin = nullptr;
     size_t pin_bytes = 0;
+    // small host calls: a mapped, coherent host buffer the kernels read and
+    // write directly (no copy in or out)
+    char* zc = nullptr;
+    char* zc_dev = nullptr;
     // the calls of this context are ordered: each waits for the previous one
     // (whatever its stream), and buffers are freed only once it is done
     hipEvent_t done_ev = nullptr;
@@ -105,6 +109,7 @@ struct qsmd_ctx {
 namespace {
 
 constexpr uint32_t kStage0wGrid = 1024;
+constexpr size_t kZeroCopyBytes = 64 * 1024;   // host calls this small run on a mapped host buffer
 constexpr uint64_t kTimingSlots = 1024;
 constexpr uint64_t kXMemoEntries = 1ull << 22;   // giant stage exact memo: 512 MB (shared by all giants of a call)
 constexpr uint32_t kTaskCap = 1u << 19;  // tasks per variant per call (beyond: searched unsplit)
@@ -268,6 +273,7 @@ void qsmd_close(qsmd_ctx* c) {
     if (c->memo) (void)hipFree(c->memo);
     if (c->io) (void)hipFree(c->io);
     if (c->pin) (void)hipHostFree(c->pin);
+    if (c->zc) (void)hipHostFree(c->zc);
     for (auto e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->done_ev) (void)hipEventDestroy(c->done_ev);
@@ -435,10 +441,15 @@ static bool lane_tables(qsmd_ctx* c, hipStream_t s, uint64_t grid) {
     return true;
 }
 
+// route (known only to the host entry, which sees the headers): kSkip0 = no
+// history fits stage 0, kSkip0w = none fits stage 0w either (every history
+// goes straight to the wide list: one wave-mode launch and the giant stage)
+enum : uint32_t { kSkip0 = 1u, kSkip0w = 2u };
+
 static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, uint64_t n_hist,
                                const qsmd_event* events, uint64_t n_events, const void* model0,
                                uint32_t flags, uint64_t max_nodes, uint8_t* status, uint64_t* nodes,
-                               uint8_t* witness, qsmd_totals* totals, hipStream_t s) {
+                               uint8_t* witness, qsmd_totals* totals, hipStream_t s, uint32_t route = 0u) {
     if (model_id != QSMD_MODEL_BANK && model_id != QSMD_MODEL_TICKET)
         return fail(c, QSMD_ERR_ARG, "unknown model_id");
     if (n_hist && (!hdr || !status)) return fail(c, QSMD_ERR_ARG, "null hdr/status");
@@ -461,7 +472,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // a long heavy list, wave mode (one search per wavefront, its DFS chain
     // ~10x shorter) for a short one -- by the last finished call's count
     const uint64_t heavy_hint = c->probe_valid ? (uint64_t)hint[1] + hint[2] : 0ull;
-    bool lane = c->heavy_mode == 1 || (c->heavy_mode == 2 && heavy_hint > c->wave_max);
+    if (c->heavy_mode == 1) route &= ~kSkip0w;   // (lane mode forced: the wide list goes on to the giant stage)
+    bool lane = !(route & kSkip0w) && (c->heavy_mode == 1 || (c->heavy_mode == 2 && heavy_hint > c->wave_max));
     // lane mode's memo tables in LDS (one wavefront per CU) when the last
     // call's heavy groups fit the CUs, else in HBM (one table per lane slot)
     const bool wide = hint[2] != 0u;   // G64 groups in the launch only when the last call had some
@@ -541,19 +553,23 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.stage0_budget = c->stage0_budget ? c->stage0_budget : ~0ull;
     const uint64_t n_groups = std::max<uint64_t>((n_hist + 63) / 64, 1);
     stage_done("start", s, cnt);
-    HIP_TRY(c, launch_compact(a0, (uint32_t)std::min<uint64_t>(n_groups, c->stage0_max_grid), s), "stage 0 launch");
+    if (!(route & kSkip0))
+        HIP_TRY(c, launch_compact(a0, (uint32_t)std::min<uint64_t>(n_groups, c->stage0_max_grid), s), "stage 0 launch");
     stage_done("stage0", s, cnt);
     HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
     // ---- stage 0w: the rest, <= 64 events (beyond: the giant stage)
     SearchArgs aw = a;
-    aw.list = l0;
-    aw.list_count = cnt + C_DEFER;
+    aw.list = (route & kSkip0) ? nullptr : l0;               // (null: every history of the batch)
+    aw.list_count = (route & kSkip0) ? nullptr : cnt + C_DEFER;
     aw.defer_list = lw;                      // (wave mode searches most of them; the rest: giants)
     aw.defer_count = cnt + C_WIDE;
     aw.heavy_list = h64;
     aw.heavy_count = cnt + C_HEAVY64;
     aw.stage0_budget = c->stage0w_budget ? c->stage0w_budget : ~0ull;
-    HIP_TRY(c, launch_compact64(aw, (uint32_t)tail_grid(2ull * c->n_cu, kStage0wGrid, hint[0]), s), "stage 0w launch");
+    if (!(route & kSkip0w))
+        HIP_TRY(c, launch_compact64(aw, (uint32_t)((route & kSkip0) ? std::min<uint64_t>(n_groups, kStage0wGrid)
+                                                                    : tail_grid(2ull * c->n_cu, kStage0wGrid, hint[0])),
+                                    s), "stage 0w launch");
     stage_done("stage0w", s, cnt);
     // ---- heavy stage: histories over the stage budgets
     const uint64_t cap = split ? 64 * c->split_budget : 0;
@@ -586,7 +602,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         wp.count32 = cnt + C_HEAVY32;
         wp.list64 = h64;
         wp.count64 = cnt + C_HEAVY64;
-        wp.list_wide = lw;
+        wp.list_wide = (route & kSkip0w) ? nullptr : lw;
         wp.count_wide = cnt + C_WIDE;
         wp.explore_cap = cap;
         wp.explore_cap_wide = split ? 16 * c->split_budget : 0;   // (the giant stage's whole-search cap)
@@ -599,7 +615,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         wp.memo_mode = (flags & QSMD_FLAG_MEMO) ? 1u : 0u;
         // LDS memo table: 8 KB per wavefront (256 entries of <= 64 events),
         // 64 KB when the last call had wide histories (1024 entries of <= 128)
-        const uint64_t wide_hint = c->probe_valid ? (uint64_t)hint[kProbeWide] : 0ull;
+        const uint64_t wide_hint = (route & kSkip0w) ? n_hist : (c->probe_valid ? (uint64_t)hint[kProbeWide] : 0ull);
         wp.buckets = wide_hint ? 256u : 32u;
         // one workgroup per history the last call sent here (+ 25 %), at
         // least 64 and at most 16 per CU (grid-stride beyond)
@@ -610,7 +626,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
                          : std::min<uint64_t>(16ull * c->n_cu,
                                               c->probe_valid ? std::max<uint64_t>(64, nh + nh / 4) : 4ull * c->n_cu);
         const uint64_t g128 = std::min<uint64_t>(16ull * c->n_cu, std::max<uint64_t>(8, wide_hint + wide_hint / 4));
-        HIP_TRY(c, launch_wave(wp, (uint32_t)g, (uint32_t)g128, s), "wave launch");
+        HIP_TRY(c, launch_wave(wp, (route & kSkip0w) ? 0u : (uint32_t)g, (uint32_t)g128, s), "wave launch");
         stage_done("wave", s, cnt);
     }
     // ---- giant stage: the split search, the combine, (the fixup), the totals
@@ -741,30 +757,58 @@ int qsmd_check_batch(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, uint64
     const size_t o_nd = o_st + align_up(n_hist, 16);
     const size_t o_tot = o_nd + align_up(n_hist * 8, 16);
     const size_t need = o_tot + align_up(sizeof(qsmd_totals), 16);
-    int rc = grow(c, &c->io, &c->io_bytes, need);
-    if (rc) return rc;
-    rc = grow_pinned(c, need);
-    if (rc) return rc;
-    if (n_hist) std::memcpy(c->pin + o_hdr, hdr, n_hist * sizeof(qsmd_hdr));
-    if (n_events) std::memcpy(c->pin + o_ev, events, n_events * sizeof(qsmd_event));
-    if (want_w) std::memset(c->pin + o_w, 0xFF, n_events);
-    auto* d_hdr = reinterpret_cast<qsmd_hdr*>(c->io + o_hdr);
-    auto* d_ev = reinterpret_cast<qsmd_event*>(c->io + o_ev);
-    auto* d_st = reinterpret_cast<uint8_t*>(c->io + o_st);
-    auto* d_nd = reinterpret_cast<uint64_t*>(c->io + o_nd);
-    auto* d_w = reinterpret_cast<uint8_t*>(c->io + o_w);
-    auto* d_tot = reinterpret_cast<qsmd_totals*>(c->io + o_tot);
-    if (o_st) HIP_TRY(c, hipMemcpyAsync(c->io, c->pin, o_st, hipMemcpyHostToDevice, s), "H2D inputs");
+    // a small call (the per-history drop-in's) runs on a mapped host buffer:
+    // the kernels read headers and events and store the outputs over the bus
+    // (plain loads and stores only), so no copy precedes or follows them
+    if (need <= kZeroCopyBytes && !c->zc) {
+        if (hipHostMalloc(reinterpret_cast<void**>(&c->zc), kZeroCopyBytes,
+                          hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&c->zc_dev), c->zc, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            if (c->zc) (void)hipHostFree(c->zc);
+            c->zc = nullptr;
+            c->zc_dev = nullptr;
+        }
+    }
+    const bool zero_copy = need <= kZeroCopyBytes && c->zc_dev != nullptr;
+    int rc = QSMD_OK;
+    if (!zero_copy) {
+        rc = grow(c, &c->io, &c->io_bytes, need);
+        if (rc) return rc;
+        rc = grow_pinned(c, need);
+        if (rc) return rc;
+    }
+    char* host = zero_copy ? c->zc : c->pin;               // the host side of the buffer
+    char* dev = zero_copy ? c->zc_dev : c->io;             // the kernels' side
+    if (n_hist) std::memcpy(host + o_hdr, hdr, n_hist * sizeof(qsmd_hdr));
+    if (n_events) std::memcpy(host + o_ev, events, n_events * sizeof(qsmd_event));
+    if (want_w) std::memset(host + o_w, 0xFF, n_events);
+    auto* d_hdr = reinterpret_cast<qsmd_hdr*>(dev + o_hdr);
+    auto* d_ev = reinterpret_cast<qsmd_event*>(dev + o_ev);
+    auto* d_st = reinterpret_cast<uint8_t*>(dev + o_st);
+    auto* d_nd = reinterpret_cast<uint64_t*>(dev + o_nd);
+    auto* d_w = reinterpret_cast<uint8_t*>(dev + o_w);
+    auto* d_tot = reinterpret_cast<qsmd_totals*>(dev + o_tot);
+    if (o_st && !zero_copy) HIP_TRY(c, hipMemcpyAsync(c->io, c->pin, o_st, hipMemcpyHostToDevice, s), "H2D inputs");
+    // routing from the headers: skip the compact stages no history fits
+    bool fits0 = false, fits0w = false;
+    for (uint64_t i = 0; i < n_hist && !fits0; ++i) {
+        const bool few = hdr[i].n_pid <= 8u;
+        fits0 = fits0 || (few && hdr[i].n_ev <= 32u);
+        fits0w = fits0w || (few && hdr[i].n_ev <= 64u);
+    }
+    const uint32_t route = n_hist == 0 ? 0u : (fits0 ? 0u : kSkip0) | (fits0w || fits0 ? 0u : kSkip0w);
     rc = check_device_locked(c, model_id, d_hdr, n_hist, d_ev, n_events, model0, flags, max_nodes, d_st, d_nd,
-                             want_w ? d_w : nullptr, d_tot, s);
+                             want_w ? d_w : nullptr, d_tot, s, route);
     if (rc) return rc;
-    HIP_TRY(c, hipMemcpyAsync(c->pin + o_w, c->io + o_w, need - o_w, hipMemcpyDeviceToHost, s), "D2H outputs");
+    if (!zero_copy)
+        HIP_TRY(c, hipMemcpyAsync(c->pin + o_w, c->io + o_w, need - o_w, hipMemcpyDeviceToHost, s), "D2H outputs");
     HIP_TRY(c, hipStreamSynchronize(s), "hipStreamSynchronize");
     c->in_flight = false;
-    if (n_hist) std::memcpy(status_out, c->pin + o_st, n_hist);
-    if (n_hist && nodes_out) std::memcpy(nodes_out, c->pin + o_nd, n_hist * 8);
-    if (want_w) std::memcpy(witness_out, c->pin + o_w, n_events);
-    if (totals_out) std::memcpy(totals_out, c->pin + o_tot, sizeof(qsmd_totals));
+    if (n_hist) std::memcpy(status_out, host + o_st, n_hist);
+    if (n_hist && nodes_out) std::memcpy(nodes_out, host + o_nd, n_hist * 8);
+    if (want_w) std::memcpy(witness_out, host + o_w, n_events);
+    if (totals_out) std::memcpy(totals_out, host + o_tot, sizeof(qsmd_totals));
     return QSMD_OK;
 }
 

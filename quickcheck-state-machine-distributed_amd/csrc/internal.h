@@ -220,7 +220,7 @@ struct WaveArgs {
     const uint32_t* count32;
     const uint32_t* list64;
     const uint32_t* count64;
-    const uint32_t* list_wide;    // stage 0w's deferred histories (> 64 events or wide values)
+    const uint32_t* list_wide;    // stage 0w's deferred histories (> 64 events or wide values); null = every history
     const uint32_t* count_wide;
     uint64_t explore_cap;         // iterations per heavy history before the giant stage (0 = none)
     uint64_t explore_cap_wide;    // the same for the wide list
@@ -235,6 +235,7 @@ struct WaveArgs {
     unsigned long long* stats;    // diagnostic: DFS iterations [max, sum], s_memtime cycles [max, sum], nodes sum,
                                   // DAG-searched histories, their s_memtime cycles max
 };
+// grid 0: no u64 launch (no history of <= 64 events in the call)
 hipError_t launch_wave(const WaveArgs& p, uint32_t grid, uint32_t grid128, hipStream_t s);
 
 // memo_search (csrc/memo.hip): per-lane search of a compact stage's heavy

@@ -432,11 +432,12 @@ __device__ __forceinline__ DagLds dag_carve(uint32_t* base, uint32_t SC, uint32_
 
 // A key's 32-bit hash: independent products folded together (a short chain)
 template <uint32_t KW>
-__device__ __forceinline__ uint32_t dag_hash(const uint32_t* kw) {
+__device__ __forceinline__ uint32_t dag_hash(const uint32_t* kw, uint32_t used) {
     constexpr uint32_t C[4] = {0x9E3779B1u, 0x85EBCA77u, 0xC2B2AE3Du, 0x27D4EB2Fu};
     uint32_t h[4] = {0x165667B1u, 0xD3A2646Cu, 0xFD7046C5u, 0xB55A4F09u};
 #pragma unroll
-    for (uint32_t k = 0; k < KW; ++k) h[k & 3u] ^= __builtin_rotateleft32(kw[k] * C[k & 3u], 5u * k);
+    for (uint32_t k = 0; k < KW; ++k)
+        if (k < used) h[k & 3u] ^= __builtin_rotateleft32(kw[k] * C[k & 3u], 5u * k);
     uint32_t x = (h[0] ^ h[1]) + (h[2] ^ h[3]);
     x ^= x >> 16;
     x *= 0x7FEB352Du;
@@ -485,9 +486,29 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
         kw[NM] = a.m0_just;
         kw[NM + 1] = (uint32_t)(int32_t)a.m0_val[0];
     }
+    // Bank: the accounts the history (or model0) can touch; the balances of
+    // the others stay 0 in every key, so the loops over key words stop at
+    // `used` (wave-uniform)
+    uint32_t n_acc = 8u, used = KW;
+    if constexpr (BANK) {
+        uint32_t touched = a.m0_exists;
+#pragma unroll
+        for (uint32_t w = 0; w < Geo<M>::NW; ++w) {
+            const uint32_t lo = d.lo[w];
+            const bool inv = d.pidv[w] != 0xFFu && !(lo & 0x80u);
+            const uint32_t bits = inv ? (1u << ((lo >> 16) & 7u)) |
+                                            (((lo >> 8) & 0xFFu) == QSMD_BANK_TRANSFER ? 1u << ((lo >> 24) & 7u) : 0u)
+                                      : 0u;
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q) touched |= __ballot((bits >> q) & 1u) ? 1u << q : 0u;
+        }
+        n_acc = touched ? 32u - (uint32_t)__builtin_clz(touched) : 1u;
+        used = NM + 1u + n_acc;
+    }
     // level boundaries in lanes: lane d of lv0 (d < 64) / lv1 (64 + d) = the first state of level d
     uint32_t lv0 = ul == 1u ? 1u : 0u, lv1 = 0u;
     uint64_t SM = 1ull;                                     // the root, in lane 0
+    uint64_t leaf_or_err = 0ull;                            // a leaf below the root or a raising step seen
     uint32_t sid = 0u;
     uint32_t n_states = 1u, n_items = 0u, nlev = 1u;
     bool fit = true;
@@ -516,33 +537,48 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
         const uint32_t deg = mpop(V);
         // the items' offsets: a prefix sum of deg over the lanes, from ballots of its bits
         uint32_t excl = 0u, total = 0u;
-        for (uint32_t b = 0; b < 8; ++b) {
-            const uint64_t bm = __ballot((deg >> b) != 0u);
-            if (!bm) break;
-            const uint64_t bb = __ballot((deg >> b) & 1u);
-            excl += lane_prefix(bb) << b;
-            total += (uint32_t)__builtin_popcountll(bb) << b;
+        if (__builtin_popcountll(SM) == 1) {                // one state: its items start the level
+            total = rl(deg, (uint32_t)__builtin_ctzll(SM));
+        } else {
+            for (uint32_t b = 0; b < 8; ++b) {
+                const uint64_t bm = __ballot((deg >> b) != 0u);
+                if (!bm) break;
+                const uint64_t bb = __ballot((deg >> b) & 1u);
+                excl += lane_prefix(bb) << b;
+                total += (uint32_t)__builtin_popcountll(bb) << b;
+            }
         }
         if (total > 64u || n_items + total > IC) { fit = false; break; }
         if (sl) L.sitem[sid] = (n_items + excl) | deg << 16;
+        leaf_or_err |= __ballot(sl && deg == 0u && sid != 0u);
         tick(0);
         if (total == 0u) break;                             // every state of the level is a leaf
         // item lane i: its state lane (the last with items at or below i), the
         // t-th candidate of that state
         const bool il = ul < total;
-        uint32_t src = 0u, e0 = 0u;
-        for (uint64_t m = SM & __ballot(deg != 0u); m; m &= m - 1ull) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(m);
-            const uint32_t e = rl(excl, l);
-            src = ul >= e ? l : src;
-            e0 = ul >= e ? e : e0;
-        }
-        uint32_t skw[KW], vw[NM];
+        const uint64_t withi = SM & __ballot(deg != 0u);
+        uint32_t skw[KW], vw[NM], e0 = 0u;
+        uint32_t vv[NM];
+        mwords(V, vv);
+        if (__builtin_popcountll(withi) == 1) {             // one state with items: its key is uniform
+            const uint32_t l = (uint32_t)__builtin_ctzll(withi);
 #pragma unroll
-        for (uint32_t k = 0; k < KW; ++k) skw[k] = (uint32_t)__shfl((int)kw[k], (int)src, 64);
-        {
-            uint32_t vv[NM];
-            mwords(V, vv);
+            for (uint32_t k = 0; k < KW; ++k) skw[k] = k < used ? rl(kw[k], l) : 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < NM; ++k) vw[k] = rl(vv[k], l);
+        } else {
+            uint32_t src = 0u;
+            for (uint64_t m = withi; m; m &= m - 1ull) {
+                const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                const uint32_t e = rl(excl, l);
+                src = ul >= e ? l : src;
+                e0 = ul >= e ? e : e0;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < KW; ++k) {
+                if (k < used) skw[k] = (uint32_t)__shfl((int)kw[k], (int)src, 64);
+                else skw[k] = 0u;
+            }
 #pragma unroll
             for (uint32_t k = 0; k < NM; ++k) vw[k] = (uint32_t)__shfl((int)vv[k], (int)src, 64);
         }
@@ -573,10 +609,12 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
             bool neg = false;
 #pragma unroll
             for (uint32_t q = 0; q < 8; ++q) {
-                const int32_t bq = (int32_t)skw[NM + 1 + q];
-                bal_a = q == ia ? bq : bal_a;
-                bal_b = q == ib ? bq : bal_b;
-                neg = neg || (((ex >> q) & 1u) && bq < 0);
+                if (q < n_acc) {
+                    const int32_t bq = (int32_t)skw[NM + 1 + q];
+                    bal_a = q == ia ? bq : bal_a;
+                    bal_b = q == ib ? bq : bal_b;
+                    neg = neg || (((ex >> q) & 1u) && bq < 0);
+                }
             }
             const uint32_t ex_a = (ex >> ia) & 1u, ex_b = (ex >> ib) & 1u;
             // post (test/Bank.hs:118-131): the invariant, then the expected response
@@ -595,10 +633,12 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
             skw[NM] = ex | ((chk ? 0u : 1u) << ia) | ((tr ? 1u : 0u) << ib);
 #pragma unroll
             for (uint32_t q = 0; q < 8; ++q) {
-                uint32_t v = skw[NM + 1 + q];
-                v = q == ia ? (uint32_t)na : v;
-                v = (tr && q == ib) ? (uint32_t)fb : v;
-                skw[NM + 1 + q] = v;
+                if (q < n_acc) {
+                    uint32_t v = skw[NM + 1 + q];
+                    v = q == ia ? (uint32_t)na : v;
+                    v = (tr && q == ib) ? (uint32_t)fb : v;
+                    skw[NM + 1 + q] = v;
+                }
             }
         } else {
             // TicketDispenser (test/TicketDispenser.hs:81-102)
@@ -621,35 +661,44 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
         // its lowest lane leads when the full keys agree; the rest (a slot
         // shared by different keys) go through a leader loop
         const bool isT = il && res == G_T;
+        leaf_or_err |= __ballot(il && res == G_ERR);
         uint32_t child = 0xFFFu;
         uint64_t LM = 0ull;
         uint64_t pending = __ballot(isT);
-        if (__builtin_popcountll(pending) > 2) {
-            const uint32_t slot = dag_hash<KW>(skw) >> 22;
-            if (isT) atomicMin(&L.tab[slot], ul);
-            __syncthreads();
-            const uint32_t w = isT ? L.tab[slot] : ul;
-            bool eq = true;
-#pragma unroll
-            for (uint32_t k = 0; k < KW; ++k) eq = eq && skw[k] == (uint32_t)__shfl((int)skw[k], (int)w, 64);
-            const bool lead = isT && w == ul;
-            LM = __ballot(lead);
-            if (isT && eq) child = n_states + (uint32_t)__builtin_popcountll(LM & ((1ull << w) - 1ull));
-            n_states += (uint32_t)__builtin_popcountll(LM);
-            if (isT) L.tab[slot] = ~0u;                     // (every lane of the slot has read it)
-            pending = __ballot(isT && !eq);
-        }
-        while (pending) {
+        // with one parent state, the first pending lane's group by direct
+        // compare (often every child: a shared pid's candidates); then hash
+        // slots when more than 2 lanes remain, then the leader loop
+        auto lead_one = [&]() {
             const uint32_t ldr = (uint32_t)__builtin_ctzll(pending);
             bool e2 = true;
 #pragma unroll
-            for (uint32_t k = 0; k < KW; ++k) e2 = e2 && skw[k] == rl(skw[k], ldr);
+            for (uint32_t k = 0; k < KW; ++k)
+                if (k < used) e2 = e2 && skw[k] == rl(skw[k], ldr);
             const uint64_t same = __ballot(e2) & pending;
             child = (same >> ul) & 1ull ? n_states : child;
             ++n_states;
             LM |= 1ull << ldr;
             pending &= ~same;
+        };
+        if (pending && __builtin_popcountll(withi) == 1) lead_one();   // (one parent: often one child)
+        if (__builtin_popcountll(pending) > 2) {
+            const bool pl = (pending >> ul) & 1ull;
+            const uint32_t slot = dag_hash<KW>(skw, used) >> 22;
+            if (pl) atomicMin(&L.tab[slot], ul);
+            __syncthreads();
+            const uint32_t w = pl ? L.tab[slot] : ul;
+            bool eq = true;
+#pragma unroll
+            for (uint32_t k = 0; k < KW; ++k)
+                if (k < used) eq = eq && skw[k] == (uint32_t)__shfl((int)skw[k], (int)w, 64);
+            const uint64_t lm = __ballot(pl && w == ul);
+            if (pl && eq) child = n_states + (uint32_t)__builtin_popcountll(lm & ((1ull << w) - 1ull));
+            n_states += (uint32_t)__builtin_popcountll(lm);
+            LM |= lm;
+            if (pl) L.tab[slot] = ~0u;                      // (every lane of the slot has read it)
+            pending = __ballot(pl && !eq);
         }
+        while (pending) lead_one();
         if (n_states > SC) { fit = false; break; }
         if (il) L.item[n_items + ul] = child | res << 12 | j << 14;
         n_items += total;
@@ -668,6 +717,14 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
     if (!fit) return -1;
 
     auto lvl_at = [&](uint32_t k) { return k < 64u ? rl(lv0, k) : rl(lv1, k - 64u); };
+    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
+    if (p.memo_mode && !leaf_or_err) {
+        // QSMD_FLAG_MEMO without a leaf or a raising step: every state fails,
+        // and the pruning DFS evaluates each state's children once: n_items
+        path_len = 0u;
+        nodes_out = (uint64_t)n_items > limit ? limit : n_items;
+        return (uint64_t)n_items > limit ? QSMD_STATUS_BUDGET : QSMD_STATUS_NONLINEARISABLE;
+    }
     // ---- backward: g of every state, deepest level first (a state's items
     // and their children's g read 4 at a time, then folded in order)
     for (int lv = (int)nlev - 1; lv >= 0; --lv) {
@@ -773,7 +830,6 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
         }
         mcount += wave_sum64(part);
     }
-    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
     const uint64_t c0 = L.glo[0] | (uint64_t)L.ghi[0] << 32;
     const uint64_t n = memo ? mcount : c0;
     __syncthreads();
@@ -1002,18 +1058,25 @@ __global__ __launch_bounds__(C_LANES) void wave_search(WaveArgs p) {
     constexpr bool W128 = Geo<M>::NW == 2;
     extern __shared__ uint32_t tab[];
     const int lane = threadIdx.x;
-    const uint32_t n32 = W128 ? 0u : *p.count32, n64 = W128 ? 0u : *p.count64, nw = *p.count_wide;
+    // (list_wide null: every history of the batch is on the wide list -- the
+    // host entry's routing when none fits the compact stages)
+    const uint32_t n32 = W128 ? 0u : *p.count32, n64 = W128 ? 0u : *p.count64;
+    const uint32_t nw = p.list_wide ? *p.count_wide : (uint32_t)p.s.n_hist;
     const uint64_t t0 = p.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     Counters cnt;
     uint32_t* dag = p.dag_states ? tab + p.buckets * 64u : nullptr;
     clear_table(tab, p.buckets, lane);
     uint32_t epoch = 0u, victim = 0u;
     for (uint32_t i = blockIdx.x; i < n32 + n64 + nw; i += gridDim.x) {
-        const uint32_t h = i < n32 ? p.list32[i] : (i < n32 + n64 ? p.list64[i - n32] : p.list_wide[i - n32 - n64]);
+        const uint32_t h = i < n32 ? p.list32[i]
+                         : (i < n32 + n64 ? p.list64[i - n32]
+                                          : (p.list_wide ? p.list_wide[i - n32 - n64] : i - n32 - n64));
         const qsmd_hdr H = p.s.hdr[h];
         const bool wide = i >= n32 + n64;
         if (wide) {
-            const bool mine = W128 ? H.n_ev > 64u : (H.n_ev <= 64u || !p.wide128);
+            // (no list: the M128 launch alone takes the batch; a <= 64-event
+            // history there has more than 8 pids and goes on to the giant stage)
+            const bool mine = W128 ? (H.n_ev > 64u || !p.list_wide) : (H.n_ev <= 64u || !p.wide128);
             if (!mine) continue;
             if (H.n_ev > (W128 || !p.wide128 ? 128u : 64u) || H.n_ev > 64u * Geo<M>::NW || H.n_pid > 8u ||
                 !p.s.m0_wave) {                  // the giant stage's
@@ -1055,8 +1118,10 @@ static hipError_t launch_one(WaveArgs p, uint32_t grid, hipStream_t s) {
 }
 
 hipError_t launch_wave(const WaveArgs& p, uint32_t grid, uint32_t grid128, hipStream_t s) {
-    hipError_t e = p.s.model_id == QSMD_MODEL_BANK ? launch_one<QSMD_MODEL_BANK, uint64_t>(p, grid, s)
-                                                   : launch_one<QSMD_MODEL_TICKET, uint64_t>(p, grid, s);
+    hipError_t e = hipSuccess;
+    if (grid)                                               // (0: no <= 64-event history in the call)
+        e = p.s.model_id == QSMD_MODEL_BANK ? launch_one<QSMD_MODEL_BANK, uint64_t>(p, grid, s)
+                                            : launch_one<QSMD_MODEL_TICKET, uint64_t>(p, grid, s);
     if (e != hipSuccess || !p.wide128) return e;
     return p.s.model_id == QSMD_MODEL_BANK ? launch_one<QSMD_MODEL_BANK, M128>(p, grid128, s)
                                            : launch_one<QSMD_MODEL_TICKET, M128>(p, grid128, s);

@@ -27,6 +27,11 @@ def main():
     args = ap.parse_args()
     h, e, _ = gen.adversarial_ticket(8, 64, bug=bool(args.bug))
     st_o, nd_o, _ = oracle_c.check_batch(1, h, e, memo=True)
+    t, k = time.perf_counter(), 0
+    while time.perf_counter() - t < 1.0:                 # the CPU point: the oracle's memo mode, 1 thread
+        oracle_c.check_batch(1, h, e, memo=True)
+        k += 1
+    print(json.dumps({"cpu_ms_per_history": round(1e3 * (time.perf_counter() - t) / k, 4), "calls": k}), flush=True)
     for case in args.cases:
         ctx = device.Context(0)
         for kv in filter(None, case.split(",")):
