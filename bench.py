@@ -30,6 +30,11 @@ import time
 # --hw-queues Q sets it for this process before torch is imported
 if "--hw-queues" in sys.argv:
     os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1]
+elif (int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("QSMD_BENCH_DIST") == "1") \
+        and "GPU_MAX_HW_QUEUES" not in os.environ:
+    # with RCCL: the 3 slot streams, the all-reduce's own stream and RCCL's
+    # internal one each keep a hardware queue (4 by default: they would share)
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "quickcheck-state-machine-distributed_amd")
@@ -83,7 +88,7 @@ class InFlight:
     of steps are all-reduced together, overlapping the next block."""
 
     def __init__(self, dev, model_id, d_hdr, n, d_ev, n_ev, S, R, flags, use_dist, knobs, budget0, streams=None,
-                 host_group=None):
+                 host_group=None, comm=None):
         self.dev, self.model_id, self.d_hdr, self.n, self.d_ev, self.n_ev = dev, model_id, d_hdr, n, d_ev, n_ev
         self.S, self.B, self.flags = S, R * S, flags
         self.ctxs = [device.Context(dev.index) for _ in range(S)]
@@ -99,7 +104,11 @@ class InFlight:
         self.tot = torch.zeros(2, self.B, 8, dtype=torch.int64, device=dev)
         self.use_dist = use_dist
         self.host_group = host_group
-        self.comm = self.streams[S - 1] if use_dist else None   # RCCL adds its own stream: reuse a slot's
+        # the all-reduce on a stream of its own: it waits for every slot's last
+        # call of the block, and no slot waits for it (a slot stream carrying
+        # it held that slot's next call behind the collective: 5.98 vs 6.68e9
+        # without the all-reduce, one rank, 60 steps)
+        self.comm = (comm or torch.cuda.Stream(dev)) if use_dist else None
         self.do_ar = use_dist and os.environ.get("QSMD_BENCH_NOAR") != "1"
         self.done = [None, None]
         self.k = 0
@@ -322,8 +331,7 @@ def main():
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="calls in flight (one context + stream each); 0 = 3 on one GPU, 2 with RCCL "
-                         "(its stream takes one of the 4 hardware queues)")
+                    help="calls in flight (one context + stream each); 0 = 3")
     ap.add_argument("--ar-rounds", type=int, default=16,
                     help="rounds of in-flight steps whose counters one RCCL all-reduce carries (N > 1)")
     ap.add_argument("--device-gen", action="store_true",
@@ -356,7 +364,8 @@ def main():
     # the slot streams, created and used before RCCL creates its own, so that
     # each gets a hardware queue of its own (GPU_MAX_HW_QUEUES)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
-    for st_ in streams:
+    comm = torch.cuda.Stream(dev) if use_dist else None
+    for st_ in streams + ([comm] if comm is not None else []):
         with torch.cuda.stream(st_):
             torch.ones(1, device=dev).add_(1)
     torch.cuda.synchronize(dev)
@@ -424,7 +433,7 @@ def main():
                 knobs.append((k, v))
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
     run = InFlight(dev, model_id, d_hdr, n, d_ev, len(ev), S, max(1, args.ar_rounds), flags, use_dist, knobs,
-                   budget0, streams, host_group)
+                   budget0, streams, host_group, comm)
     elapsed = run.timed(args.steps, args.warmup)
     s0_ms, call_ms = run.ctxs[0].timing_read()
     st, nd, tot = run.results()

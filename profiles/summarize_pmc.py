@@ -3,7 +3,9 @@ and PMC counters of the dominant search kernel (stage 0), over the LAST
 `--last` dispatches of that kernel -- bench.py's roofline leg, the
 synchronous calls it times after its timed region -- so that the profile's
 mean duration is the one bench.py's `roofline.kernel_ms.mean` divides by.
-The whole-run rocprofv3 --stats table is kept beside it (`kernels`).
+The whole-run rocprofv3 --stats table is kept beside it (`kernels`; its
+means include the launches that ran beside other calls in flight), and every
+kernel's stats over the roofline leg alone (`roofline_leg_kernels`).
 
 HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are
 collected in separate passes, are in KiB, and on gfx950 FETCH_SIZE reports
@@ -50,6 +52,23 @@ def durations(out_dir, last):
     return d, d[-last:] if last else d
 
 
+def leg_kernels(out_dir, last):
+    """Per-kernel stats over the roofline leg only: every dispatch from the
+    first of the last `last` stage-0 dispatches on (synchronous calls, one
+    at a time: each kernel's mean is its per-launch work time)."""
+    tr = rows(os.path.join(out_dir, "trace", "**", "*kernel_trace.csv"))
+    dom = sorted((r for r in tr if is_dominant(r["Kernel_Name"])), key=lambda r: int(r["Start_Timestamp"]))
+    if not dom or not last:
+        return {}
+    t0 = int(dom[-last]["Start_Timestamp"])
+    per = defaultdict(list)
+    for r in tr:
+        if int(r["Start_Timestamp"]) >= t0:
+            per[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return {k: {"calls": len(v), "mean_ns": statistics.mean(v), "median_ns": statistics.median(v),
+                "min_ns": min(v), "max_ns": max(v)} for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
+
+
 def counters(out_dir, name, last):
     per = defaultdict(lambda: defaultdict(float))   # dispatch -> counter -> value
     for r in rows(os.path.join(out_dir, name, "**", "*counter_collection.csv")):
@@ -73,6 +92,7 @@ def main():
     stats = rows(os.path.join(out_dir, "trace", "**", "*kernel_stats.csv"))
     res["kernels"] = {r["Name"]: {"calls": int(r["Calls"]), "mean_ns": float(r["AverageNs"]),
                                   "pct": float(r["Percentage"])} for r in stats}
+    res["roofline_leg_kernels"] = leg_kernels(out_dir, args.last)
     all_d, d = durations(out_dir, args.last)
     if d:
         res["dominant"] = {"dispatches": len(d), "mean_ns": statistics.mean(d), "median_ns": statistics.median(d),

@@ -200,11 +200,12 @@ def test_lane_mode(ctx, knobs, name, n, budget, max_nodes, entries, lds):
 
 @pytest.mark.parametrize("name,n,budget,max_nodes", LANE_CASES)
 @pytest.mark.parametrize("min_rem,grid,dag", [(4, 0, 128), (4, 0, 0), (0, 0, 0), (64, 0, 0), (0, 7, 0),
-                                              (4, 7, 128), (4, 0, 6), (4, 0, 4095)])  # (4095: cut to the LDS)
+                                              (4, 7, 128), (4, 0, 6), (4, 0, 24),
+                                              (4, 0, 4095)])  # (4095: cut to the LDS)
 def test_wave_mode(ctx, knobs, name, n, budget, max_nodes, min_rem, grid, dag):
     """Wave mode of the heavy stage (csrc/wave.hip): one wavefront per
-    history; the state DAG (dag: its capacity in states; 0 = off, 6 = most
-    histories overflow it mid-build and run the DFS) or the DFS in
+    history; the state DAG (dag: its capacity in states; 0 = off, 6 / 24 =
+    many histories overflow it mid-build and run the DFS) or the DFS in
     wave-uniform registers with the exact-count memo in an 8-way LDS table
     per wavefront.  min_rem: memo only above this many remaining events (64:
     no memo at all, 0: at every node); grid 7: few wavefronts, many
