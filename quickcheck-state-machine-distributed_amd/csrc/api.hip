@@ -541,7 +541,6 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
 
     c->ws_dirty = true;                 // until the giant stage is enqueued
     hipEvent_t* evs = &c->ev[3 * (c->n_calls % kTimingSlots)];
-    HIP_TRY(c, hipEventRecord(evs[0], s), "hipEventRecord");
     // ---- stage 0: every history, <= 32 events
     SearchArgs a0 = a;
     a0.list = nullptr;
@@ -553,10 +552,14 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.stage0_budget = c->stage0_budget ? c->stage0_budget : ~0ull;
     const uint64_t n_groups = std::max<uint64_t>((n_hist + 63) / 64, 1);
     stage_done("start", s, cnt);
-    if (!(route & kSkip0))
-        HIP_TRY(c, launch_compact(a0, (uint32_t)std::min<uint64_t>(n_groups, c->stage0_max_grid), s), "stage 0 launch");
+    if (!(route & kSkip0)) {           // (the events at the kernel's start and end)
+        HIP_TRY(c, launch_compact(a0, (uint32_t)std::min<uint64_t>(n_groups, c->stage0_max_grid), s, evs[0], evs[1]),
+                "stage 0 launch");
+    } else {
+        HIP_TRY(c, hipEventRecord(evs[0], s), "hipEventRecord");
+        HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
+    }
     stage_done("stage0", s, cnt);
-    HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
     // ---- stage 0w: the rest, <= 64 events (beyond: the giant stage)
     SearchArgs aw = a;
     aw.list = (route & kSkip0) ? nullptr : l0;               // (null: every history of the batch)

@@ -25,6 +25,7 @@
 // to the heavy list (csrc/memo.hip searches it with the exact-count memo).
 // Histories outside the stage's bounds go to the next stage through a
 // wave-aggregated append to the defer list.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "internal.h"
@@ -161,11 +162,15 @@ hipError_t launch_compact64(const SearchArgs& a, uint32_t grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_compact(const SearchArgs& a, uint32_t grid, hipStream_t s) {
+// start / stop: events the launch itself records at the kernel's start and
+// end (the per-call stage-0 timing: no launch gap inside the interval)
+hipError_t launch_compact(const SearchArgs& a, uint32_t grid, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
     if (a.model_id == QSMD_MODEL_BANK)
-        hipLaunchKernelGGL((compact_search<QSMD_MODEL_BANK, G32>), dim3(grid), dim3(C_LANES), 0, s, a);
+        hipExtLaunchKernelGGL((compact_search<QSMD_MODEL_BANK, G32>), dim3(grid), dim3(C_LANES), 0, s, start, stop,
+                              0u, a);
     else
-        hipLaunchKernelGGL((compact_search<QSMD_MODEL_TICKET, G32>), dim3(grid), dim3(C_LANES), 0, s, a);
+        hipExtLaunchKernelGGL((compact_search<QSMD_MODEL_TICKET, G32>), dim3(grid), dim3(C_LANES), 0, s, start, stop,
+                              0u, a);
     return hipGetLastError();
 }
 

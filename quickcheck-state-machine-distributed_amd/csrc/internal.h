@@ -279,8 +279,9 @@ __device__ __forceinline__ void bucket_add(unsigned long long* buckets, uint32_t
                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Stage 0 (csrc/compact.hip): <= 32 events, <= 8 pids, 19-bit values.
-hipError_t launch_compact(const SearchArgs& a, uint32_t grid, hipStream_t s);
+// Stage 0 (csrc/compact.hip): <= 32 events, <= 8 pids, 19-bit values; the
+// launch records `start` / `stop` at the kernel's start and end.
+hipError_t launch_compact(const SearchArgs& a, uint32_t grid, hipStream_t s, hipEvent_t start, hipEvent_t stop);
 // Stage 0w (csrc/compact.hip, G64): <= 64 events, <= 8 pids, 13/25-bit values, list mode.
 hipError_t launch_compact64(const SearchArgs& a, uint32_t grid, hipStream_t s);
 
