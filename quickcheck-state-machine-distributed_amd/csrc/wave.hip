@@ -521,6 +521,14 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
             tprev = t;
         }
     };
+    auto flush_stats = [&](uint32_t levels) {               // (the diagnostic counters, lane 0)
+        tick(4);
+        if (timing && ul == 0) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) atomicAdd(p.stats + 8 + k, (unsigned long long)tph[k]);
+            atomicAdd(p.stats + 13, (unsigned long long)levels);
+        }
+    };
     while (true) {
         // state lanes: the candidates with a response (takeInvocations, findResponse)
         const bool sl = (SM >> ul) & 1ull;
@@ -722,6 +730,7 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
         // QSMD_FLAG_MEMO without a leaf or a raising step: every state fails,
         // and the pruning DFS evaluates each state's children once: n_items
         path_len = 0u;
+        flush_stats(nlev);
         nodes_out = (uint64_t)n_items > limit ? limit : n_items;
         return (uint64_t)n_items > limit ? QSMD_STATUS_BUDGET : QSMD_STATUS_NONLINEARISABLE;
     }
@@ -833,12 +842,7 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
     const uint64_t c0 = L.glo[0] | (uint64_t)L.ghi[0] << 32;
     const uint64_t n = memo ? mcount : c0;
     __syncthreads();
-    tick(4);
-    if (timing && ul == 0) {
-#pragma unroll
-        for (int k = 0; k < 5; ++k) atomicAdd(p.stats + 8 + k, (unsigned long long)tph[k]);
-        atomicAdd(p.stats + 13, (unsigned long long)nlev);
-    }
+    flush_stats(nlev);
     if ((!memo && (f0 & G_SAT)) || n > limit) {
         nodes_out = limit;
         return QSMD_STATUS_BUDGET;
