@@ -227,10 +227,12 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *                       last finished call's heavy histories fit one
  *                       workgroup per CU, else in HBM; 0: always HBM (an
  *                       LDS-table workgroup holds a CU); 2: always LDS
+ *   "memo_lds_entries"  the LDS tables' entries per lane, a power of two in
+ *                       4..64 (default 64: 128 KB per workgroup; 16: 32 KB)
  *   "memo_grid", "memo_lane_entries"  lane mode: workgroups at most (0 = 12
  *                       per CU), entries per lane (HBM tables: grid x 64 x
  *                       entries x 96 B, grown on demand; the LDS tables hold
- *                       min(64, entries))
+ *                       min(memo_lds_entries, entries))
  *   "wave_grid"         wave mode workgroups (0 = the last call's heavy count
  *                       + 25 %, at most 16 per CU; grid-stride beyond)
  *   "wave_min_rem"      wave mode: no memo probe at nodes with at most this

@@ -85,6 +85,7 @@ struct qsmd_ctx {
     // lane mode's tables: one per lane slot of the memo grid
     uint64_t memo_grid = 0;            // heavy stage (lane mode): workgroups at most (0 = 12 per CU); one table each
     uint64_t mt_entries = 128;
+    uint32_t memo_lds_entries = 64;             // LDS tables: entries per lane (power of two, 4..64)
     char* mt = nullptr;
     size_t mt_bytes = 0;
     uint32_t mt_epoch = 0;
@@ -329,6 +330,10 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->memo_stats = reinterpret_cast<unsigned long long*>(value);
     } else if (n == "memo_stats_groups") {
         c->memo_stats_groups = value;
+    } else if (n == "memo_lds_entries") {
+        if (value < 4 || value > 64 || (value & (value - 1)))
+            return fail(c, QSMD_ERR_ARG, "memo_lds_entries: a power of two in 4..64");
+        c->memo_lds_entries = (uint32_t)value;
     } else if (n == "memo_lds") {
         if (value > 2) return fail(c, QSMD_ERR_ARG, "memo_lds: 0 = HBM tables, 1 = LDS for short lists, 2 = LDS");
         c->memo_lds = (uint32_t)value;
@@ -589,6 +594,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].s.list_count = cnt + (w ? C_HEAVY64 : C_HEAVY32);
             mp[w].table = reinterpret_cast<uint32_t*>(c->mt + (w ? slots * 32 : 0));
             mp[w].entries = (uint32_t)c->mt_entries;
+            mp[w].lds_entries = (uint32_t)std::min<uint64_t>(c->memo_lds_entries, c->mt_entries);
             mp[w].epoch = c->mt_epoch;
             mp[w].giant_cap = cap;
             mp[w].stats = c->memo_stats;

@@ -115,7 +115,8 @@ __device__ __forceinline__ void memo_insert(uint32_t* tab, const MemoKey<MODEL, 
 // per lane, word w of entry e at col[(e * 8 + w) * 64] (each lane its own
 // bank); an LDS probe instead of an HBM round trip per node.  128 KB per
 // workgroup: one wavefront per CU, chosen only when the heavy groups fit
-// the CUs (api.hip).  Word 0 holds the history index; kNoHistory = empty.
+// the CUs (api.hip); fewer entries per lane (knob memo_lds_entries) leave
+// the CU's LDS to other work.  Word 0 holds the history index; kNoHistory = empty.
 constexpr uint32_t kLdsEntries = 64;
 constexpr uint32_t kNoHistory = 0xFFFFFFFFu;
 
@@ -228,7 +229,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
     uint32_t mask;
     if constexpr (LT) {
         tab = lcol;
-        mask = (p.entries < kLdsEntries ? p.entries : kLdsEntries) - 1u;
+        mask = p.lds_entries - 1u;
     } else {
         tab = p.table + ((uint64_t)blockIdx.x * C_LANES + (uint64_t)lane) * (uint64_t)p.entries *
                             (uint64_t)MemoEntry<G>::W;
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32,
     uint32_t* lcol = nullptr;
     if constexpr (LT) {
         lcol = lds + sizeof(MemoLds<MODEL, G32>) / 4u + lane;
-        for (uint32_t e = 0; e < kLdsEntries; ++e) lcol[e * 8u * C_LANES] = kNoHistory;
+        for (uint32_t e = 0; e < p32.lds_entries; ++e) lcol[e * 8u * C_LANES] = kNoHistory;
     }
     // stage 0w's wide list goes on to the giant stage (wave mode searches it)
     const uint32_t nf = *p32.fwd_count;
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32,
 template <uint32_t MODEL, bool LT>
 static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s,
                                 bool* lds_refused = nullptr) {
-    const size_t lds = LT ? sizeof(MemoLds<MODEL, G32>) + (size_t)kLdsEntries * 8u * C_LANES * 4u
+    const size_t lds = LT ? sizeof(MemoLds<MODEL, G32>) + (size_t)p32.lds_entries * 8u * C_LANES * 4u
                           : (wide ? sizeof(MemoLds<MODEL, G64>) : sizeof(MemoLds<MODEL, G32>));
     if constexpr (LT) {   // beyond the default 64 KB of dynamic LDS (set on every launch: per device)
         const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&memo_search<MODEL, true>),

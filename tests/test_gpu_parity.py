@@ -97,7 +97,7 @@ def test_random_any_shape(ctx, model):
 
 DEFAULTS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
             "wave_grid": 0, "split_budget": 1024, "memo_lane_entries": 128, "memo_grid": 0, "split_xmemo": 1,
-            "memo_lds": 1, "dag_states": 128}
+            "memo_lds": 1, "memo_lds_entries": 64, "dag_states": 128}
 
 
 @pytest.fixture
@@ -187,13 +187,15 @@ LANE_CASES = [("bank_4x16_bugs", 50000, 64, 0), ("bank_4x16_bugs", 20000, 8, 300
 
 @pytest.mark.parametrize("name,n,budget,max_nodes", LANE_CASES)
 @pytest.mark.parametrize("entries", [128, 2])
-@pytest.mark.parametrize("lds", [0, 2])
-def test_lane_mode(ctx, knobs, name, n, budget, max_nodes, entries, lds):
+@pytest.mark.parametrize("lds,lds_entries", [(0, 64), (2, 64), (2, 16)])
+def test_lane_mode(ctx, knobs, name, n, budget, max_nodes, entries, lds, lds_entries):
     """Lane mode of the heavy stage (exact-count state memo in a private
-    table per lane, in HBM or, lds=2, in LDS): verdicts, node counts and
-    witnesses must equal the reference's.  2 entries: constant replacement;
-    max_nodes: the budget falls inside reused subtrees."""
-    knobs(heavy_mode=1, memo_lane_entries=entries, stage0_budget=budget, stage0w_budget=budget, memo_lds=lds)
+    table per lane, in HBM or, lds=2, in LDS with 64 or 16 entries per
+    lane): verdicts, node counts and witnesses must equal the reference's.
+    2 entries: constant replacement; max_nodes: the budget falls inside
+    reused subtrees."""
+    knobs(heavy_mode=1, memo_lane_entries=entries, stage0_budget=budget, stage0w_budget=budget, memo_lds=lds,
+          memo_lds_entries=lds_entries)
     hdr, ev, _ = gen.generate_config(name, 5, n)
     _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
 
