@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "qsmd.h"
 #include "qsmd_gen.h"
 
@@ -292,5 +294,23 @@ hipError_t launch_compact64(const SearchArgs& a, uint32_t grid, hipStream_t s);
 hipError_t launch_giants(const SplitArgs& p, uint32_t grid, hipStream_t s);
 hipError_t launch_frontier_only(int variant, const SplitArgs& p, hipStream_t s);
 hipError_t launch_tasks_only(int variant, const SplitArgs& p, uint32_t grid, hipStream_t s);
+
+// A kernel's dynamic-LDS limit (hipFuncAttributeMaxDynamicSharedMemorySize)
+// raised once per device to the largest size launched so far: the
+// attribute persists, and setting it before every launch cost host time on
+// the per-call path.  `cache`: one slot per device, zero-initialised.
+constexpr int kAttrDevices = 64;
+inline hipError_t ensure_dyn_lds(const void* fn, std::atomic<int>* cache, size_t lds) {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kAttrDevices) dev = -1;
+    if (dev >= 0 && cache[dev].load(std::memory_order_relaxed) >= (int)lds) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e == hipSuccess && dev >= 0) {
+        int cur = cache[dev].load(std::memory_order_relaxed);
+        while (cur < (int)lds && !cache[dev].compare_exchange_weak(cur, (int)lds)) {
+        }
+    }
+    return e;
+}
 
 }  // namespace qsmd

@@ -111,13 +111,12 @@ __device__ __forceinline__ void memo_insert(uint32_t* tab, const MemoKey<MODEL, 
     if constexpr (G::EV == 64) e[2] = make_uint4(k.rem_hi, 0u, 0u, 0u);
 }
 
-// The LDS table (G32, a short heavy list): kLdsEntries direct-mapped entries
+// The LDS table (G32, a short heavy list): lds_entries (<= 64) direct-mapped entries
 // per lane, word w of entry e at col[(e * 8 + w) * 64] (each lane its own
 // bank); an LDS probe instead of an HBM round trip per node.  128 KB per
 // workgroup: one wavefront per CU, chosen only when the heavy groups fit
 // the CUs (api.hip); fewer entries per lane (knob memo_lds_entries) leave
 // the CU's LDS to other work.  Word 0 holds the history index; kNoHistory = empty.
-constexpr uint32_t kLdsEntries = 64;
 constexpr uint32_t kNoHistory = 0xFFFFFFFFu;
 
 template <uint32_t MODEL, class G>
@@ -368,8 +367,8 @@ static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32
     const size_t lds = LT ? sizeof(MemoLds<MODEL, G32>) + (size_t)p32.lds_entries * 8u * C_LANES * 4u
                           : (wide ? sizeof(MemoLds<MODEL, G64>) : sizeof(MemoLds<MODEL, G32>));
     if constexpr (LT) {   // beyond the default 64 KB of dynamic LDS (set on every launch: per device)
-        const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&memo_search<MODEL, true>),
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        static std::atomic<int> set[kAttrDevices];
+        const hipError_t attr = ensure_dyn_lds(reinterpret_cast<const void*>(&memo_search<MODEL, true>), set, lds);
         if (attr != hipSuccess) {
             if (lds_refused) *lds_refused = true;
             return attr;

@@ -1046,7 +1046,9 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
 }
 
 __device__ __forceinline__ void clear_table(uint32_t* tab, uint32_t buckets, int lane) {
-    for (uint32_t b = 0; b < buckets; ++b) tab[b * 64u + (uint32_t)lane] = 0xFFFFFFFFu;   // word 2 never matches
+    // every word 0xFFFFFFFF (word 2 never matches), 16 B per lane and store
+    uint4* t4 = reinterpret_cast<uint4*>(tab);
+    for (uint32_t k = (uint32_t)lane; k < buckets * 16u; k += 64u) t4[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
 }
 
 }  // namespace
@@ -1113,8 +1115,8 @@ static hipError_t launch_one(WaveArgs p, uint32_t grid, hipStream_t s) {
     }
     const size_t lds = wave_lds<MODEL, M>(p);
     if (lds > 64u * 1024u) {
-        const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wave_search<MODEL, M>),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        static std::atomic<int> set[kAttrDevices];
+        const hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&wave_search<MODEL, M>), set, lds);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL((wave_search<MODEL, M>), dim3(grid), dim3(C_LANES), lds, s, p);

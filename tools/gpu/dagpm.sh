@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_split.py -x -q --timeout 120 \
-    --timeout-method thread -k "wave_mode or heavy_any_shape or generated_configs or memo or stage_cascade or adversarial or dag" \
+    --timeout-method thread -k "wave_mode or heavy_any_shape or generated_configs or memo or stage_cascade or adversarial or dag or lane_mode" \
     > gpurun_out/pm_pytest.log 2>&1 &&
 timeout -k 10 300 python -u tools/stress_parity.py --batches 20 --seed 53 --knobs --wide > gpurun_out/pm_stress.log 2>&1 &&
 timeout -k 10 120 python -u tools/config4.py --reps 40 "" > gpurun_out/pm_c4.log 2>&1 &&
