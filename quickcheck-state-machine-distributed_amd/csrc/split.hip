@@ -835,7 +835,7 @@ __device__ __forceinline__ uint32_t ld_cnt(const uint32_t* c) { return poll_u32(
 
 // The call's last act: totals from the buckets, the probe snapshot for the
 // host, every counter and bucket restored for the next call.
-__device__ void finish_call(const SplitArgs& p, int lane) {
+__device__ __forceinline__ void finish_call(const SplitArgs& p, int lane) {
     unsigned long long* bk = p.s.buckets;
     unsigned long long* xb = bk + (size_t)kBuckets * kBucketWords;   // early-exit recount
     const unsigned long long* src = p.early ? xb : bk;
@@ -879,17 +879,16 @@ __device__ __forceinline__ void beat(const SplitArgs& p, int lane, uint32_t k, u
         __hip_atomic_store(p.debug + (uint64_t)blockIdx.x * 4 + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The giant stage's work (a call with giants or the early exit): out of
+// line, so that a call without giants -- nearly every call -- runs the
+// kernel's short path alone (the functions below take the arguments by
+// reference; from the kernel's own parameter that made a private copy of
+// them, ~400 B per lane, at every launch)
 template <uint32_t MODEL>
-__global__ __launch_bounds__(64) void giant_search(SplitArgs p) {
-    __shared__ GiantLds<MODEL> u;
+__device__ __noinline__ void giant_work(const SplitArgs& p, uint32_t n_g, GiantLds<MODEL>& u) {
     const SearchArgs& a = p.s;
     const int lane = threadIdx.x;
     uint32_t* cnt = p.cnt;
-    const uint32_t n_g = ld_cnt(cnt + C_GIANT);
-    if (n_g == 0 && !p.early) {                 // nothing to do but the totals
-        if (blockIdx.x == 0) finish_call(p, lane);
-        return;
-    }
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     beat(p, lane, 0, 1);
     // ---- frontier: chunks of 64 giants; variant 0 on all lanes, then variant
@@ -996,6 +995,22 @@ __global__ __launch_bounds__(64) void giant_search(SplitArgs p) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         finish_call(p, lane);
     }
+}
+
+template <uint32_t MODEL>
+__global__ __launch_bounds__(64) void giant_search(SplitArgs p) {
+    __shared__ GiantLds<MODEL> u;
+    const int lane = threadIdx.x;
+    const uint32_t n_g = ld_cnt(p.cnt + C_GIANT);
+    if (n_g == 0 && !p.early) {                 // nothing to do but the totals
+        if (blockIdx.x == 0) finish_call(p, lane);
+        return;
+    }
+    // the arguments where the launch put them (the kernel's one argument, at
+    // offset 0 of the kernarg segment): no private copy of them
+    // (a constant-address-space pointer: the same 64-bit global address)
+    const SplitArgs* kp = reinterpret_cast<const SplitArgs*>((uintptr_t)__builtin_amdgcn_kernarg_segment_ptr());
+    giant_work<MODEL>(*kp, n_g, u);
 }
 
 // qsmd_split_frontier: one giant (giant_list[0]), one lane.
