@@ -129,6 +129,14 @@ def _ptr(arr):
     return None if arr is None else ctypes.c_void_p(arr.ctypes.data)
 
 
+# The host entry's CPython fast path (csrc/pyfast.c: the buffers through the
+# buffer protocol, one C call of qsmd_check_batch); without it, ctypes.
+try:
+    from . import _pyfast
+except ImportError:
+    _pyfast = None
+
+
 class Context:
     """One context per GPU (one process per GPU)."""
 
@@ -140,6 +148,7 @@ class Context:
             raise DeviceError(f"qsmd_open(device={device}) failed with {rc}: no usable HIP device")
         self._h = h
         self._lib = lib
+        self._check_fn = ctypes.cast(lib.qsmd_check_batch, ctypes.c_void_p).value
         if time_limit_ms is not None:
             lib.qsmd_set_time_limit_ms(h, int(time_limit_ms))
 
@@ -178,12 +187,17 @@ class Context:
         if witness:
             flags |= QSMD_FLAG_WITNESS
         tot = Totals()
-        m0 = ctypes.cast(ctypes.pointer(model0), ctypes.c_void_p) if model0 is not None else None
-        rc = self._lib.qsmd_check_batch(
-            self._h, model_id, _ptr(hdr) if n else None, n,
-            _ptr(events) if len(events) else None, len(events), m0, flags, max_nodes,
-            _ptr(status) if n else None, _ptr(nodes) if n else None,
-            _ptr(wit) if (wit is not None and len(events)) else None, ctypes.byref(tot))
+        if _pyfast is not None:
+            rc = _pyfast.check_batch(self._check_fn, (self._h.value or 0) if self._h else 0, model_id, hdr, events,
+                                     ctypes.addressof(model0) if model0 is not None else 0, flags, max_nodes,
+                                     status, nodes, wit, tot)
+        else:
+            m0 = ctypes.cast(ctypes.pointer(model0), ctypes.c_void_p) if model0 is not None else None
+            rc = self._lib.qsmd_check_batch(
+                self._h, model_id, _ptr(hdr) if n else None, n,
+                _ptr(events) if len(events) else None, len(events), m0, flags, max_nodes,
+                _ptr(status) if n else None, _ptr(nodes) if n else None,
+                _ptr(wit) if (wit is not None and len(events)) else None, ctypes.byref(tot))
         self._check(rc, "qsmd_check_batch")
         return status, nodes, wit, tot.as_dict()
 

@@ -39,6 +39,28 @@ def test_abi_exports_every_declared_symbol():
     assert device.load_library().qsmd_abi_version() == 2
 
 
+def test_fast_host_entry_forwards_to_the_c_abi():
+    """The binding's CPython fast path (csrc/pyfast.c) is built and is only a
+    forwarder: on a NULL context it returns the C ABI's own QSMD_ERR_ARG, like
+    the ctypes call; buffers that are not include/qsmd.h records are refused
+    before any call."""
+    from qsmd import _pyfast
+    lib = device.load_library()
+    fn = ctypes.cast(lib.qsmd_check_batch, ctypes.c_void_p).value
+    hdr, ev, _ = gen.generate_config("ticket_2x10", 0, 4)
+    st, nd, tot = np.empty(4, np.uint8), np.empty(4, np.uint64), device.Totals()
+    rc_c = lib.qsmd_check_batch(None, models.MODEL_TICKET, hdr.ctypes.data, 4, ev.ctypes.data, len(ev), None, 1, 0,
+                                st.ctypes.data, nd.ctypes.data, None, ctypes.byref(tot))
+    rc_f = _pyfast.check_batch(fn, 0, models.MODEL_TICKET, hdr, ev, 0, 1, 0, st, nd, None, tot)
+    assert rc_c == rc_f == -1
+    with pytest.raises(ValueError):
+        _pyfast.check_batch(fn, 0, 1, hdr, ev.view(np.uint8)[:12], 0, 1, 0, st, nd, None, tot)
+    with pytest.raises(ValueError):
+        _pyfast.check_batch(fn, 0, 1, hdr, ev, 0, 1, 0, st[:2], nd, None, tot)
+    with pytest.raises(TypeError):
+        _pyfast.check_batch(fn, 0, 1, hdr, ev, 0, 1, 0, st, nd, None, b"read-only")
+
+
 def test_gen_abi_exports():
     lib = ctypes.CDLL(gen.LIB_PATH)
     for n in _declared("qsmd_gen.h"):
