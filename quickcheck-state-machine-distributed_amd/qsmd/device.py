@@ -188,9 +188,9 @@ class Context:
             flags |= QSMD_FLAG_WITNESS
         tot = Totals()
         if _pyfast is not None:
-            rc = _pyfast.check_batch(self._check_fn, (self._h.value or 0) if self._h else 0, model_id, hdr, events,
-                                     ctypes.addressof(model0) if model0 is not None else 0, flags, max_nodes,
-                                     status, nodes, wit, tot)
+            rc = _pyfast.check_batch(self._check_fn, (self._h.value or 0) if self._h else 0, int(model_id), hdr,
+                                     events, ctypes.addressof(model0) if model0 is not None else 0, int(flags),
+                                     int(max_nodes), status, nodes, wit, tot)
         else:
             m0 = ctypes.cast(ctypes.pointer(model0), ctypes.c_void_p) if model0 is not None else None
             rc = self._lib.qsmd_check_batch(
