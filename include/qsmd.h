@@ -377,7 +377,8 @@ int qsmd_wellformed_batch_device(qsmd_ctx* ctx, const qsmd_hdr* hdr_dev, uint64_
 int qsmd_last_kernel_ms(qsmd_ctx* ctx, float* ms_out);
 
 /* Per-call device timings since the last reset (at most the last 1024 calls):
- * stage0_ms[i] = the first (dominant) search kernel, call_ms[i] = every
+ * stage0_ms[i] = the first (dominant) search kernel (0 when the host entry
+ * skipped stage 0: no history of the call fitted it), call_ms[i] = every
  * kernel of call i.  Synchronises on the recorded events. */
 int qsmd_timing_reset(qsmd_ctx* ctx);
 int qsmd_timing_read(qsmd_ctx* ctx, float* stage0_ms, float* call_ms, uint64_t max,

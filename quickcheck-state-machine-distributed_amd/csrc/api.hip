@@ -56,6 +56,7 @@ struct qsmd_ctx {
     // timing: per call, events before stage 0, after stage 0 and after the
     // giant stage, recorded on the launch stream (a ring of kTimingSlots)
     std::vector<hipEvent_t> ev;        // 3 per slot
+    std::vector<uint8_t> ev_no0;       // per slot: stage 0 skipped (its end event not recorded)
     uint64_t n_calls = 0;              // calls recorded since the last reset
     bool timed = false;
     uint64_t time_limit_ms = 120000;   // safety net per search launch
@@ -246,6 +247,7 @@ int qsmd_open(qsmd_ctx** out, int device) {
         return QSMD_ERR_DEVICE;
     }
     c->ev.resize(3 * kTimingSlots, nullptr);
+    c->ev_no0.assign(kTimingSlots, 0);
     for (auto& e : c->ev) {
         if (hipEventCreate(&e) != hipSuccess) { qsmd_close(c); return QSMD_ERR_DEVICE; }
     }
@@ -560,10 +562,10 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     if (!(route & kSkip0)) {           // (the events at the kernel's start and end)
         HIP_TRY(c, launch_compact(a0, (uint32_t)std::min<uint64_t>(n_groups, c->stage0_max_grid), s, evs[0], evs[1]),
                 "stage 0 launch");
-    } else {
+    } else {                           // (no stage-0 end event: one packet less before the first kernel)
         HIP_TRY(c, hipEventRecord(evs[0], s), "hipEventRecord");
-        HIP_TRY(c, hipEventRecord(evs[1], s), "hipEventRecord");
     }
+    c->ev_no0[c->n_calls % kTimingSlots] = (route & kSkip0) ? 1u : 0u;
     stage_done("stage0", s, cnt);
     // ---- stage 0w: the rest, <= 64 events (beyond: the giant stage)
     SearchArgs aw = a;
@@ -927,7 +929,10 @@ int qsmd_timing_read(qsmd_ctx* c, float* stage0_ms, float* call_ms, uint64_t max
     for (uint64_t i = 0; i < n; ++i) {
         hipEvent_t* evs = &c->ev[3 * ((first + i) % kTimingSlots)];
         HIP_TRY(c, hipEventSynchronize(evs[2]), "hipEventSynchronize");
-        if (stage0_ms) HIP_TRY(c, hipEventElapsedTime(&stage0_ms[i], evs[0], evs[1]), "elapsed");
+        if (stage0_ms) {
+            if (c->ev_no0[(first + i) % kTimingSlots]) stage0_ms[i] = 0.0f;   // (no stage 0 in that call)
+            else HIP_TRY(c, hipEventElapsedTime(&stage0_ms[i], evs[0], evs[1]), "elapsed");
+        }
         if (call_ms) HIP_TRY(c, hipEventElapsedTime(&call_ms[i], evs[0], evs[2]), "elapsed");
     }
     *n_out = n;
