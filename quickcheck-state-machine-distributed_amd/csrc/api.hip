@@ -75,6 +75,7 @@ struct qsmd_ctx {
     uint32_t memo_lds = 1;                      // heavy-stage memo tables in LDS: 0 never, 1 short lists, 2 always
     uint64_t giant_grid = 0;           // giant stage workgroups (0 = 2 per CU)
     uint64_t giant_stall_us = 0;       // diagnostic: the giant stage's first frontier chunk starts this late
+    unsigned long long* s0_stamps = nullptr;    // diagnostic (stage0_stamps_ptr): 8 x u64 per stage-0 workgroup
     // heavy stage: one wavefront per history (wave_search, csrc/wave.hip)
     // unless the last finished call sent more than wave_max histories there
     // (then one lane per history, memo_search, csrc/memo.hip); heavy_mode
@@ -87,6 +88,7 @@ struct qsmd_ctx {
     uint64_t memo_grid = 0;            // heavy stage (lane mode): workgroups at most (0 = 12 per CU); one table each
     uint64_t mt_entries = 128;
     uint32_t memo_lds_entries = 64;             // LDS tables: entries per lane (power of two, 4..64)
+    uint64_t memo_lds_cap = 0;                  // diagnostic: LDS-table bytes accepted at most (0 = the device's)
     char* mt = nullptr;
     size_t mt_bytes = 0;
     uint32_t mt_epoch = 0;
@@ -322,6 +324,8 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->dag_states = value;
     } else if (n == "dag_debug_ptr") {      // diagnostic: device buffer (16 + DAG LDS words) for one history
         c->dag_dbg = reinterpret_cast<uint32_t*>(value);
+    } else if (n == "stage0_stamps_ptr") {  // diagnostic build (QSMD_DIAG_STAGE0=2): 8 x u64 per workgroup
+        c->s0_stamps = reinterpret_cast<unsigned long long*>(value);
     } else if (n == "dag_debug_hist") {
         c->dag_dbg_h = value;
     } else if (n == "wave_min_rem") {
@@ -336,6 +340,8 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         if (value < 4 || value > 64 || (value & (value - 1)))
             return fail(c, QSMD_ERR_ARG, "memo_lds_entries: a power of two in 4..64");
         c->memo_lds_entries = (uint32_t)value;
+    } else if (n == "memo_lds_cap") {       // diagnostic: force the LDS-refused path (the HBM tables)
+        c->memo_lds_cap = value;
     } else if (n == "memo_lds") {
         if (value > 2) return fail(c, QSMD_ERR_ARG, "memo_lds: 0 = HBM tables, 1 = LDS for short lists, 2 = LDS");
         c->memo_lds = (uint32_t)value;
@@ -485,7 +491,10 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // call's heavy groups fit the CUs, else in HBM (one table per lane slot)
     const bool wide = hint[2] != 0u;   // G64 groups in the launch only when the last call had some
     const uint64_t g32 = c->probe_valid ? ((uint64_t)hint[1] + 63u) / 64u : ~0ull;
-    const bool lt = c->memo_lds == 2 || (c->memo_lds == 1 && g32 <= (uint64_t)c->n_cu);
+    bool lt = c->memo_lds == 2 || (c->memo_lds == 1 && g32 <= (uint64_t)c->n_cu);
+    // (an LDS size the device refuses: the HBM tables, allocated below)
+    const uint32_t lds_entries = (uint32_t)std::min<uint64_t>(c->memo_lds_entries, c->mt_entries);
+    if (lane && lt && !wide && !memo_lds_accepted(model_id, lds_entries, c->memo_lds_cap)) lt = false;
     // (LDS tables: one workgroup per CU, so no idle workgroups beyond
     // twice the groups expected -- they would hold CUs the next call's
     // stage 0 could use)
@@ -557,6 +566,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.heavy_list = h32;
     a0.heavy_count = cnt + C_HEAVY32;
     a0.stage0_budget = c->stage0_budget ? c->stage0_budget : ~0ull;
+    a0.stamps = c->s0_stamps;
     const uint64_t n_groups = std::max<uint64_t>((n_hist + 63) / 64, 1);
     stage_done("start", s, cnt);
     if (!(route & kSkip0)) {           // (the events at the kernel's start and end)
@@ -596,7 +606,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].s.list_count = cnt + (w ? C_HEAVY64 : C_HEAVY32);
             mp[w].table = reinterpret_cast<uint32_t*>(c->mt + (w ? slots * 32 : 0));
             mp[w].entries = (uint32_t)c->mt_entries;
-            mp[w].lds_entries = (uint32_t)std::min<uint64_t>(c->memo_lds_entries, c->mt_entries);
+            mp[w].lds_entries = lds_entries;
             mp[w].epoch = c->mt_epoch;
             mp[w].giant_cap = cap;
             mp[w].stats = c->memo_stats;
@@ -811,7 +821,12 @@ int qsmd_check_batch(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, uint64
     const uint32_t route = n_hist == 0 ? 0u : (fits0 ? 0u : kSkip0) | (fits0w || fits0 ? 0u : kSkip0w);
     rc = check_device_locked(c, model_id, d_hdr, n_hist, d_ev, n_events, model0, flags, max_nodes, d_st, d_nd,
                              want_w ? d_w : nullptr, d_tot, s, route);
-    if (rc) return rc;
+    if (rc) {
+        // kernels enqueued before the failure may still read the inputs and
+        // write the outputs in zc / pin: done before the next call writes there
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
     if (!zero_copy)
         HIP_TRY(c, hipMemcpyAsync(c->pin + o_w, c->io + o_w, need - o_w, hipMemcpyDeviceToHost, s), "D2H outputs");
     HIP_TRY(c, hipStreamSynchronize(s), "hipStreamSynchronize");

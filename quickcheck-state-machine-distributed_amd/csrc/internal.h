@@ -111,6 +111,10 @@ struct SearchArgs {
     // histories a stage hands on to the giant stage (split search)
     uint32_t* giant_list;
     uint32_t* giant_count;
+    // diagnostic build only (QSMD_DIAG_STAGE0=2, stage0_stamps_ptr): stage 0
+    // writes 8 x u64 per group (compact.hip: phase stamps, DFS iterations,
+    // the workgroup's entry and exit)
+    unsigned long long* stamps;
 };
 
 // qsmd_ctx::probe_host slots: [C_DEFER, C_HEAVY32, C_HEAVY64, C_GIANT,
@@ -255,9 +259,11 @@ struct MemoArgs {
     const uint32_t* fwd_list;     // appended to s.giant_list as they are (stage 0w's wide list)
     const uint32_t* fwd_count;
 };
-// lds_tables: the G32 memo tables in LDS (ignored with `wide`)
+// lds_tables: the G32 memo tables in LDS (ignored with `wide`; only after
+// memo_lds_accepted said yes for p32.lds_entries)
 hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool lds_tables,
                        hipStream_t s);
+bool memo_lds_accepted(uint32_t model_id, uint32_t lds_entries, size_t cap);
 
 hipError_t launch_gen(const qsmd_gen_params& p, uint64_t first, uint64_t n_hist, uint32_t ev_base, qsmd_hdr* hdr,
                       qsmd_event* events, uint8_t* bug_out, hipStream_t s);

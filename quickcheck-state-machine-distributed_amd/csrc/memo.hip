@@ -361,35 +361,45 @@ __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32,
     cnt.flush(p32.s.buckets, lane);
 }
 
+template <uint32_t MODEL>
+static size_t memo_lds_bytes(uint32_t lds_entries) {
+    return sizeof(MemoLds<MODEL, G32>) + (size_t)lds_entries * 8u * C_LANES * 4u;
+}
+
 template <uint32_t MODEL, bool LT>
-static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s,
-                                bool* lds_refused = nullptr) {
-    const size_t lds = LT ? sizeof(MemoLds<MODEL, G32>) + (size_t)p32.lds_entries * 8u * C_LANES * 4u
+static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s) {
+    const size_t lds = LT ? memo_lds_bytes<MODEL>(p32.lds_entries)
                           : (wide ? sizeof(MemoLds<MODEL, G64>) : sizeof(MemoLds<MODEL, G32>));
-    if constexpr (LT) {   // beyond the default 64 KB of dynamic LDS (set on every launch: per device)
-        static std::atomic<int> set[kAttrDevices];
-        const hipError_t attr = ensure_dyn_lds(reinterpret_cast<const void*>(&memo_search<MODEL, true>), set, lds);
-        if (attr != hipSuccess) {
-            if (lds_refused) *lds_refused = true;
-            return attr;
-        }
-    }
     hipLaunchKernelGGL((memo_search<MODEL, LT>), dim3(grid), dim3(C_LANES), lds, s, p32, p64, wide ? 1u : 0u);
     return hipGetLastError();
 }
 
+// Whether the LDS tables of `lds_entries` per lane can launch: their size
+// within `cap` (0 = the device's limit; a lower cap is a diagnostic knob,
+// memo_lds_cap, that makes the refusal happen on gfx950) and the kernel's
+// dynamic-LDS limit raised to it.  The host decides before it sizes the
+// tables, so a refusal runs the HBM tables it then allocates.
+bool memo_lds_accepted(uint32_t model_id, uint32_t lds_entries, size_t cap) {
+    const bool bank = model_id == QSMD_MODEL_BANK;
+    const size_t lds = bank ? memo_lds_bytes<QSMD_MODEL_BANK>(lds_entries) : memo_lds_bytes<QSMD_MODEL_TICKET>(lds_entries);
+    if (cap && lds > cap) return false;
+    static std::atomic<int> set_b[kAttrDevices], set_t[kAttrDevices];
+    const hipError_t e = bank ? ensure_dyn_lds(reinterpret_cast<const void*>(&memo_search<QSMD_MODEL_BANK, true>), set_b, lds)
+                              : ensure_dyn_lds(reinterpret_cast<const void*>(&memo_search<QSMD_MODEL_TICKET, true>), set_t, lds);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return true;
+}
+
+// lds_tables (with !wide): the caller has checked memo_lds_accepted
 hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool lds_tables,
                        hipStream_t s) {
     const bool bank = p32.s.model_id == QSMD_MODEL_BANK;
-    if (lds_tables && !wide) {
-        bool refused = false;
-        const hipError_t e = bank ? launch_memo_t<QSMD_MODEL_BANK, true>(p32, p64, grid, wide, s, &refused)
-                                  : launch_memo_t<QSMD_MODEL_TICKET, true>(p32, p64, grid, wide, s, &refused);
-        if (!refused) return e;
-        // the device refused the LDS size (hipFuncSetAttribute): the HBM
-        // tables give the same results
-        (void)hipGetLastError();
-    }
+    if (lds_tables && !wide)
+        return bank ? launch_memo_t<QSMD_MODEL_BANK, true>(p32, p64, grid, wide, s)
+                    : launch_memo_t<QSMD_MODEL_TICKET, true>(p32, p64, grid, wide, s);
     return bank ? launch_memo_t<QSMD_MODEL_BANK, false>(p32, p64, grid, wide, s)
                 : launch_memo_t<QSMD_MODEL_TICKET, false>(p32, p64, grid, wide, s);
 }

@@ -1084,6 +1084,18 @@ __global__ __launch_bounds__(C_LANES) void wave_search(WaveArgs p) {
             // history there has more than 8 pids and goes on to the giant stage)
             const bool mine = W128 ? (H.n_ev > 64u || !p.list_wide) : (H.n_ev <= 64u || !p.wide128);
             if (!mine) continue;
+            // the batch unlisted: no compact stage checked the header (the
+            // wide list's come validated by stage 0w); a wrong model or an
+            // event range outside the batch is ENCODE_ERROR, never read
+            if (!p.list_wide && H.n_ev <= QSMD_MAX_EVENTS && H.n_pid <= QSMD_MAX_PIDS &&
+                (H.model_id != MODEL || (uint64_t)H.ev_off + H.n_ev > p.s.n_events)) {
+                if (lane == 0) {
+                    p.s.status[h] = (uint8_t)QSMD_STATUS_ENCODE_ERROR;
+                    if (p.s.nodes) p.s.nodes[h] = 0ull;
+                    cnt.add(QSMD_STATUS_ENCODE_ERROR, 0ull);
+                }
+                continue;
+            }
             if (H.n_ev > (W128 || !p.wide128 ? 128u : 64u) || H.n_ev > 64u * Geo<M>::NW || H.n_pid > 8u ||
                 !p.s.m0_wave) {                  // the giant stage's
                 if (lane == 0) p.s.giant_list[atomicAdd(p.s.giant_count, 1u)] = h;

@@ -4,7 +4,9 @@ Histories are independent, so a batch is split into contiguous shards, one
 per rank (one process per GPU); no data moves between ranks during the
 search.  The only collective is one all-reduce of the qsmd_totals counters
 (SUM) -- over RCCL/xGMI on the GPUs (torch.distributed "nccl" backend), over
-gloo in the CPU tests -- plus a MAX of the early-stop flag.
+gloo in the CPU tests -- plus the early-stop flag: with early exit, a MIN
+of the first failing history's index after every chunk, so ranks stop
+searching once every history left to them lies after it.
 
 The per-rank checker is a callable so the same driver runs the HIP search on
 a GPU (``device_checker``) and is exercised on CPU with gloo in the tests.
@@ -70,14 +72,24 @@ def _collective_device(group=None):
     return torch.device("cpu")
 
 
-def check_sharded(checker, gen_params, n_total, rank, world, group=None):
+def check_sharded(checker, gen_params, n_total, rank, world, group=None, early_exit=False, chunk=65536):
     """Generate this rank's shard of a seeded synthetic stream, check it with
     ``checker(model_id, hdr, events) -> (status, nodes)`` and all-reduce the
-    totals.  Returns (global totals, (first, count), status, nodes)."""
+    totals.  Returns (global totals, stop flag, (first, count), status, nodes).
+
+    ``early_exit``: QuickCheck's stop at the first failing test
+    (/root/reference/test/TicketDispenser.hs:284-322, ``expectFailure``)
+    across ranks -- see check_shard_early_exit; the checker is then called
+    as ``checker(model_id, hdr, events, early=True)``."""
     from . import gen
 
     first, count = shard(n_total, rank, world)
     hdr, events, _ = gen.generate(gen_params, first, count)
+    if early_exit:
+        status, nodes, info = check_shard_early_exit(checker, gen_params.model_id, hdr, events, n_total, rank,
+                                                     world, chunk=chunk, group=group)
+        tot, _ = allreduce_totals(totals_from_status(status, nodes), 0, group)
+        return tot, int(info["first_fail"] < n_total), (first, count), status, nodes
     status, nodes = checker(gen_params.model_id, hdr, events)
     local = totals_from_status(status, nodes)
     stop = int((np.asarray(status) == 0).any() or (np.asarray(status) == 2).any())
@@ -85,10 +97,86 @@ def check_sharded(checker, gen_params, n_total, rank, world, group=None):
     return tot, stop, (first, count), status, nodes
 
 
+def chunk_slice(hdr, events, a, b):
+    """Histories [a, b) of a batch as a batch of their own: headers rebased
+    onto the events they span (one copy of those events per chunk, not of
+    the shard's)."""
+    h = np.array(hdr[a:b], copy=True)
+    if len(h) == 0:
+        return h, events[:0]
+    lo = int(h["ev_off"].min())
+    hi = int((h["ev_off"].astype(np.int64) + h["n_ev"].astype(np.int64)).max())
+    h["ev_off"] -= lo
+    return h, events[lo:hi]
+
+
+def check_shard_early_exit(checker, model_id, hdr, events, n_total, rank, world, chunk=65536, group=None):
+    """QSMD_FLAG_EARLY_EXIT_BATCH over a sharded batch ("a MAX
+    on the early-stop flag"; here the flag carries the smallest global index
+    of a failing history, a MIN all-reduce).
+
+    Each rank checks its contiguous shard in chunks of ``chunk`` histories,
+    each with the device's early exit (everything after the chunk's first
+    non-linearisable or raising history is SKIPPED).  After every chunk one
+    MIN all-reduce publishes the global index of the first failing history
+    found so far; a rank stops once its next chunk starts after it.  Every
+    rank runs the same number of rounds (each computes every rank's chunk
+    schedule, so all take the same decision to stop).  Afterwards the
+    histories after the global first failure are SKIPPED with 0 nodes, so
+    status, nodes and totals equal one context's QSMD_FLAG_EARLY_EXIT_BATCH
+    over the concatenated batch: every history up to the first failure is
+    searched in full (its chunk started before it, and a chunk only skips
+    after its own first failure, which is never earlier).
+
+    Returns (status, nodes, info) for this rank's shard; info holds the
+    global first failure (n_total if none), the rounds and the histories
+    this rank searched (not SKIPPED by the device, in chunks it ran)."""
+    import torch.distributed as dist
+
+    first, count = shard(n_total, rank, world)
+    assert len(hdr) == count
+    status = np.full(count, 5, dtype=np.uint8)                 # SKIPPED until searched
+    nodes = np.zeros(count, dtype=np.uint64)
+    starts = [shard(n_total, r, world) for r in range(world)]  # (first, count) of every rank
+    rounds_all = max((c + chunk - 1) // chunk for _, c in starts) if n_total else 0
+    best = n_total                                             # global first failure (none: n_total)
+    searched = 0
+    rounds = 0
+    for k in range(rounds_all):
+        # does any rank still have a chunk that starts before the first failure?
+        if not any(k * chunk < c and f + k * chunk < best for f, c in starts):
+            break
+        local = best
+        a = k * chunk
+        if a < count and first + a < best:
+            b = min(count, a + chunk)
+            h, e = chunk_slice(hdr, events, a, b)
+            st, nd = checker(model_id, h, e, early=True)
+            st = np.asarray(st, dtype=np.uint8)
+            status[a:b] = st
+            nodes[a:b] = np.asarray(nd, dtype=np.uint64)
+            searched += int((st != 5).sum())
+            fails = np.nonzero((st == 0) | (st == 2))[0]
+            if len(fails):
+                local = min(local, first + a + int(fails[0]))
+        best = int(_allreduce(np.array([local]), dist.ReduceOp.MIN, group)[0])
+        rounds += 1
+    cut = best - first                                         # local index of the global first failure
+    if cut < count:
+        after = max(0, cut + 1)
+        status[after:] = 5
+        nodes[after:] = 0
+    return status, nodes, dict(first_fail=best, rounds=rounds, searched=searched)
+
+
 def device_checker(ctx, max_nodes=0):
-    """Checker running the HIP search through the C ABI (host buffers)."""
-    def run(model_id, hdr, events):
-        st, nd, _, _ = ctx.check_arrays(model_id, hdr, events, max_nodes=max_nodes)
+    """Checker running the HIP search through the C ABI (host buffers);
+    early=True adds QSMD_FLAG_EARLY_EXIT_BATCH."""
+    from . import device
+
+    def run(model_id, hdr, events, early=False):
+        flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_EARLY_EXIT_BATCH if early else 0)
+        st, nd, _, _ = ctx.check_arrays(model_id, hdr, events, flags=flags, max_nodes=max_nodes)
         return st, nd
     return run
 

@@ -89,6 +89,106 @@ def test_two_rank_gloo_equals_single_process(config):
 
 
 # ---------------------------------------------------------------------------
+# Early termination across ranks (QSMD_FLAG_EARLY_EXIT_BATCH on a sharded
+# batch): the result equals one context's early exit over the
+# concatenated batch, and the ranks search fewer histories than without it.
+
+def early_exit_reference(st, nd):
+    """One context's QSMD_FLAG_EARLY_EXIT_BATCH from full results: every
+    history after the first non-linearisable or raising one is SKIPPED with 0
+    nodes (include/qsmd.h; the device's semantics, tests/test_gpu_parity.py::
+    test_early_exit_batch)."""
+    st = np.array(st, dtype=np.uint8, copy=True)
+    nd = np.array(nd, dtype=np.uint64, copy=True)
+    fails = np.nonzero((st == 0) | (st == 2))[0]
+    if len(fails):
+        st[fails[0] + 1:] = 5
+        nd[fails[0] + 1:] = 0
+    return st, nd
+
+
+def _oracle_early_checker(model_id, hdr, events, early=False):
+    st, nd = _oracle_checker(model_id, hdr, events)
+    return early_exit_reference(st, nd) if early else (st, nd)
+
+
+def planted_stream(config, n_total, plant):
+    """The generated stream with one failing history planted at index
+    `plant` (a linearisable config: its only failure)."""
+    from qsmd import gen
+    hdr, ev, _ = gen.generate(gen.params(**gen.CONFIGS[config]), 0, n_total)
+    if plant is not None:
+        ev = ev.copy()
+        o, n = int(hdr[plant]["ev_off"]), int(hdr[plant]["n_ev"])
+        resp = [k for k in range(o, o + n) if ev["kp"][k] & 0x80]
+        k = resp[-1]                                  # the last response: a value nothing else can explain
+        ev["code"][k] = 7                             # Balance
+        ev["val"][k] = 1 << 20
+    return hdr, ev
+
+
+def _early_worker(rank, world, port, config, n_total, plant, chunk, out_q):
+    sys.path[:0] = [os.path.join(HERE, "..", "quickcheck-state-machine-distributed_amd"),
+                    os.path.join(HERE, "..", "oracle"), HERE]
+    import torch.distributed as dist
+
+    from qsmd import dist as qdist
+    from qsmd import gen
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hdr, ev = planted_stream(config, n_total, plant)
+        first, count = qdist.shard(n_total, rank, world)
+        h, e = qdist.chunk_slice(hdr, ev, first, first + count)
+        st, nd, info = qdist.check_shard_early_exit(_oracle_early_checker, gen.CONFIGS[config]["model_id"], h, e,
+                                                    n_total, rank, world, chunk=chunk)
+        tot, _ = qdist.allreduce_totals(qdist.totals_from_status(st, nd))
+        out_q.put((rank, st.tolist(), [int(x) for x in nd], info, tot.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("config,plant,chunk", [("bank_4x16_bugs", None, 200), ("bank_4x16", 2300, 256),
+                                                ("bank_4x16", 700, 128), ("bank_4x16", None, 500)])
+def test_two_rank_gloo_early_exit(config, plant, chunk):
+    from qsmd import dist as qdist
+    from qsmd import gen
+
+    world, n_total = 2, 3001
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_early_worker, args=(r, world, port, config, n_total, plant, chunk, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict((r[0], r[1:]) for r in (q.get(timeout=240) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    hdr, ev = planted_stream(config, n_total, plant)
+    st_full, nd_full = _oracle_checker(gen.CONFIGS[config]["model_id"], hdr, ev)
+    st_ref, nd_ref = early_exit_reference(st_full, nd_full)
+    cat_st = np.array(results[0][0] + results[1][0], dtype=np.uint8)
+    cat_nd = np.array(results[0][1] + results[1][1], dtype=np.uint64)
+    assert np.array_equal(cat_st, st_ref) and np.array_equal(cat_nd, nd_ref)
+    assert results[0][3] == results[1][3] == qdist.totals_from_status(st_ref, nd_ref).tolist()
+    fails = np.nonzero((st_full == 0) | (st_full == 2))[0]
+    first_fail = int(fails[0]) if len(fails) else n_total
+    assert results[0][2]["first_fail"] == results[1][2]["first_fail"] == first_fail
+    searched = results[0][2]["searched"] + results[1][2]["searched"]
+    assert results[0][2]["rounds"] == results[1][2]["rounds"]        # the same collectives on every rank
+    if first_fail < n_total:
+        assert first_fail + 1 <= searched < n_total  # everything up to the failure, and less than all
+        if first_fail < 1500:                        # in rank 0's shard: rank 1 stops once it is known
+            assert results[1][2]["searched"] <= (first_fail // chunk + 1) * chunk
+    else:
+        assert searched == n_total
+
+
+# ---------------------------------------------------------------------------
 # One history split across ranks (SURVEY.md §8e): frontier in DFS order,
 # round-robin tasks, MIN all-reduce of the first deciding task, SUM gather,
 # ordered fold (qsmd_combine_tasks of the C ABI, host code).

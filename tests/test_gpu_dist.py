@@ -83,10 +83,34 @@ def _worker(rank, world, port, n_total, out_q):
                                                      flags=device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_MEMO)
         res["one_round"] = (int(s), None if w is None else [int(x) for x in w], info["searched_here"],
                             info["n_tasks"], info["rounds"])
+        # QSMD_FLAG_EARLY_EXIT_BATCH over the shards (chunks, MIN all-reduce
+        # of the first failure); rank 0 also runs one context's early exit over
+        # the concatenated batch
+        from test_distributed import planted_stream
+        ee = []
+        for config, plant in EARLY_CASES:
+            hdr, ev = planted_stream(config, n_total, plant)
+            mid = gen.CONFIGS[config]["model_id"]
+            first, count = qdist.shard(n_total, rank, world)
+            h, e = qdist.chunk_slice(hdr, ev, first, first + count)
+            st, nd, info = qdist.check_shard_early_exit(qdist.device_checker(ctx, max_nodes=10**7), mid, h, e,
+                                                        n_total, rank, world, chunk=2048)
+            one = None
+            if rank == 0:
+                st1, nd1, _, tot1 = ctx.check_arrays(mid, hdr, ev, max_nodes=10**7, flags=device.QSMD_FLAG_EXHAUSTIVE |
+                                                     device.QSMD_FLAG_EARLY_EXIT_BATCH)
+                one = (st1.tolist(), [int(x) for x in nd1], tot1)
+            ee.append((st.tolist(), [int(x) for x in nd], info, one))
+        res["early"] = ee
         out_q.put((rank, res))
     finally:
         ctx.close()
         dist.destroy_process_group()
+
+
+# (config, planted failure): the generated bugs (a failure near the start),
+# one failure deep in rank 1's shard, one in rank 0's
+EARLY_CASES = [("bank_4x16_bugs", None), ("bank_4x16", 14000), ("bank_4x16", 6500)]
 
 
 def test_two_processes_on_the_hip_kernels():
@@ -142,3 +166,18 @@ def test_two_processes_on_the_hip_kernels():
         assert results[r]["one_round"][1] == results[r]["split"][4][2]
         assert results[r]["one_round"][4] == 1
     assert results[0]["one_round"][3] > 2 * world and early < full, (early, full)
+    # sharded early exit == one context's early exit over the whole batch,
+    # with fewer histories searched than the batch (without the flag: all)
+    for j, (config, plant) in enumerate(EARLY_CASES):
+        cat_st = np.array(results[0]["early"][j][0] + results[1]["early"][j][0], dtype=np.uint8)
+        cat_nd = np.array(results[0]["early"][j][1] + results[1]["early"][j][1], dtype=np.uint64)
+        st1, nd1, tot1 = results[0]["early"][j][3]
+        assert np.array_equal(cat_st, np.array(st1, dtype=np.uint8)), config
+        assert np.array_equal(cat_nd, np.array(nd1, dtype=np.uint64)), config
+        assert qdist.totals_from_status(cat_st, cat_nd).tolist()[:8] == [
+            tot1[k] for k in ("checked", "linearisable", "nonlinearisable", "model_errors", "encode_errors",
+                              "budget", "skipped", "nodes")]
+        ff = results[0]["early"][j][2]["first_fail"]
+        assert ff == results[1]["early"][j][2]["first_fail"] < n_total
+        searched = results[0]["early"][j][2]["searched"] + results[1]["early"][j][2]["searched"]
+        assert ff + 1 <= searched < n_total, (config, plant, searched)

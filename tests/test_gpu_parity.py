@@ -95,9 +95,9 @@ def test_random_any_shape(ctx, model):
     _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
 
 
-DEFAULTS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
+DEFAULTS = {"stage0_budget": 32, "stage0_grid": 65536, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
             "wave_grid": 0, "split_budget": 1024, "memo_lane_entries": 128, "memo_grid": 0, "split_xmemo": 1,
-            "memo_lds": 1, "memo_lds_entries": 64, "dag_states": 128}
+            "memo_lds": 1, "memo_lds_entries": 64, "dag_states": 128, "memo_lds_cap": 0}
 
 
 @pytest.fixture
@@ -166,6 +166,17 @@ def test_mixed_sizes_one_batch(ctx):
 
 @pytest.mark.parametrize("name,n", [("ticket_2x10", 20000), ("bank_4x16", 50000),
                                     ("bank_4x16_bugs", 50000), ("bank_6x24", 20000)])
+@pytest.mark.parametrize("grid", [3, 77])
+def test_stage0_grids(ctx, knobs, name, n, grid):
+    """Stage 0 with fewer workgroups than groups (grid-stride: 3 workgroups
+    take every group, 77 an uneven share each): the same results."""
+    knobs(stage0_grid=grid)
+    hdr, ev, _ = gen.generate_config(name, 3, n)
+    _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+
+
+@pytest.mark.parametrize("name,n", [("ticket_2x10", 20000), ("bank_4x16", 50000),
+                                    ("bank_4x16_bugs", 50000), ("bank_6x24", 20000)])
 @pytest.mark.parametrize("budget", [0, 8, 32])
 @pytest.mark.parametrize("heavy", [0, 1])
 def test_generated_configs(ctx, knobs, name, n, budget, heavy):
@@ -217,6 +228,22 @@ def test_wave_mode(ctx, knobs, name, n, budget, max_nodes, min_rem, grid, dag):
           dag_states=dag)
     hdr, ev, _ = gen.generate_config(name, 6, n)
     _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
+
+
+@pytest.mark.parametrize("memo_lds", [1, 2])
+def test_lds_tables_refused_run_hbm_tables(ctx, knobs, memo_lds):
+    """Lane mode asks for LDS memo tables (memo_lds 2: always; 1: the short
+    heavy list of a config-2 batch at the library's budget) and the device
+    refuses the size (memo_lds_cap below it, the diagnostic knob): the call
+    runs the HBM tables it then allocates.  Fresh memo_grid, so no table
+    from an earlier test is there to be reused."""
+    knobs(heavy_mode=1, memo_lds=memo_lds, memo_grid=37, memo_lds_cap=1024, stage0_budget=16)
+    hdr, ev, _ = gen.generate_config("bank_4x16", 9, 50000)
+    for _ in range(2):                    # (the second call: the hint-sized grid)
+        st, _, _ = _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**7)
+    assert (st == codec.STATUS_LIN).all()
+    hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 9, 50000)
+    _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**7)
 
 
 def test_lane_tables_too_large_fall_back_to_wave_mode(ctx, knobs):
@@ -453,6 +480,34 @@ def test_encode_errors(ctx):
     st, nd, _, tot = ctx.check_arrays(models.MODEL_BANK, hdr, ev)
     assert list(st) == [3, 3, 3, 3, 1]
     assert tot["encode_errors"] == 4
+
+
+@pytest.mark.parametrize("model", ["bank", "ticket"])
+def test_host_entry_wide_only_bad_headers(ctx, knobs, model):
+    """A host-entry batch with no history of <= 64 events skips the compact
+    stages (the wave kernel's M128 launch takes the batch unlisted), so no
+    compact stage validates the headers there: a wrong model_id and event
+    ranges outside the batch must still be ENCODE_ERROR (nodes 0), never
+    searched or read, and every other history the oracle's result."""
+    knobs(heavy_mode=2)
+    rng = random.Random(77 if model == "bank" else 78)
+    m = models.BY_NAME[model]
+    hs = [histgen.wellformed_history(rng, model, rng.randint(33, 64), rng.randint(2, 8), p_pending=0.0)
+          for _ in range(48)]
+    b = codec.encode(m, hs)
+    hdr = b.hdr.copy()
+    assert (hdr["n_ev"] > 64).all()
+    other = models.MODEL_TICKET if m.model_id == models.MODEL_BANK else models.MODEL_BANK
+    hdr["model_id"][3] = other                         # wrong model
+    hdr["ev_off"][7] = len(b.events) - 10              # runs past the batch's events
+    hdr["ev_off"][11] = 0x7FFFFFF0                     # far outside
+    bad = [3, 7, 11]
+    st, nd, _, tot = ctx.check_arrays(m.model_id, hdr, b.events, max_nodes=200000)
+    assert (st[bad] == codec.STATUS_ENCODE_ERROR).all() and (nd[bad] == 0).all()
+    good = np.setdiff1d(np.arange(len(hdr)), bad)
+    st_o, nd_o, _ = oracle_c.check_batch(m.model_id, b.hdr, b.events, max_nodes=200000, threads=8)
+    assert np.array_equal(st[good], st_o[good]) and np.array_equal(nd[good], nd_o[good])
+    assert tot["encode_errors"] == len(bad)
 
 
 # BASELINE.json configs at their single-GPU sizes: config 1 (TicketDispenser
