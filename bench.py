@@ -485,7 +485,9 @@ def main():
     out = {
         "metric": METRIC, "value": value, "unit": "histories/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+        "dtype_note": ("exact integer search: stage 0 holds invocation values in 14 bits, responses in 25, "
+                       "balances in int32; wider values go on to the int64 stages; node counts u64"),
         "data": "synthetic (seeded scheduler-policy generator, include/qsmd_gen.h" +
                 (", generated on the GPU)" if args.device_gen else ")"),
         "config": {"workload": args.config, "histories_per_gpu": n,

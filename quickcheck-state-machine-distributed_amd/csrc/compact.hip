@@ -43,6 +43,10 @@
 #ifndef QSMD_DIAG_L2
 #define QSMD_DIAG_L2 0
 #endif
+// QSMD_DIAG_SEARCH2=1: every search twice (its marginal cost)
+#ifndef QSMD_DIAG_SEARCH2
+#define QSMD_DIAG_SEARCH2 0
+#endif
 
 namespace qsmd {
 
@@ -115,7 +119,7 @@ __device__ __forceinline__ int stage_fresh(const SearchArgs& a, bool fresh, uint
     const bool packed = F != 0ull && __ballot(fresh && !lane_uni) == 0ull && N0 > 0u;
     if (packed) stage_packed<MODEL, G>(a, N0, off0, (uint32_t)__builtin_popcountll(F), s_ev, lane);
     else if (small) stage_lane<MODEL, G>(a, H, s_ev, lane);
-    if (small) finish_lane<G>(s_ev, lane, n_ev, n_pid, s);
+    if (small) finish_lane<MODEL, G>(s_ev, lane, n_ev, n_pid, a.events + H.ev_off, s);
     s.ok = s.ok && enc_ok;
 
     const bool defer = enc_ok && (!small || (s.ok && !s.fits));
@@ -141,7 +145,8 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
 
     const int lane = threadIdx.x;
     const uint64_t total = a.list ? (uint64_t)*a.list_count : a.n_hist;
-    Counters cnt;
+    if ((uint64_t)blockIdx.x * C_LANES >= total) return;   // (stage 0w of a call that deferred nothing)
+    WaveCounters cnt;
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t user_limit = a.max_nodes ? a.max_nodes : ~0ull;
     const bool tiered = a.stage0_budget < user_limit && a.heavy_list != nullptr;
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
         const uint64_t ts0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
         int status = stage_fresh<MODEL, G>(a, active, h, s_ev, s_bal, lane, dfs, H);
-        if (status == -2) continue;
+        const bool live = status != -2;     // (-2: no history here, or handed to the next stage)
 #if QSMD_DIAG_STAGE0 == 1
         if (status == -1) status = QSMD_STATUS_LINEARISABLE;   // diagnostic build: no search
 #endif
@@ -182,6 +187,18 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
                 a.stamps[g * 8 + lane] = v;
             }
         }
+#elif QSMD_DIAG_SEARCH2
+        // diagnostic build: every search runs twice (the second from the same
+        // initial state), to price the search's marginal cost
+        if (search) {
+            const LaneDFS<MODEL, G> d0 = dfs;
+            status = run_search(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
+            dfs = d0;
+            if constexpr (MODEL == QSMD_MODEL_BANK)
+                for (int q = 0; q < QSMD_BANK_MAX_ACCOUNTS; ++q)
+                    s_bal[q][lane] = ((a.m0_exists >> q) & 1u) ? (int32_t)a.m0_val[q] : 0;
+            status = run_search(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
+        }
 #else
         // the general path (pid masks): finish_lane does not pair (lane.h)
         if (search) status = run_search(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
@@ -190,12 +207,13 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
         // over the stage budget (not the caller's): searched again by the heavy stage
         const bool heavy = tiered && status == QSMD_STATUS_BUDGET && dfs.nodes >= limit;
         wave_append(heavy, h, a.heavy_list, a.heavy_count, lane);
-        if (heavy) continue;
-
-        a.status[h] = (uint8_t)status;
-        if (a.nodes) a.nodes[h] = dfs.nodes;
-        if (a.witness && status == QSMD_STATUS_LINEARISABLE) dfs.write_witness(a.witness + H.ev_off, n_ev);
-        cnt.add(status, dfs.nodes);
+        const bool out = live && !heavy;
+        if (out) {
+            a.status[h] = (uint8_t)status;
+            if (a.nodes) a.nodes[h] = dfs.nodes;
+            if (a.witness && status == QSMD_STATUS_LINEARISABLE) dfs.write_witness(a.witness + H.ev_off, n_ev);
+        }
+        cnt.add(out, status, dfs.nodes);    // (every lane: the status counts are ballots)
     }
     cnt.flush(a.buckets, lane);
 #if QSMD_DIAG_STAGE0 == 2

@@ -24,13 +24,20 @@ constexpr int C_CHUNK = 16;
 constexpr int32_t V19_MIN = -(1 << 18), V19_MAX = (1 << 18) - 1;   // model0 values (api.hip m0_small)
 
 // compressed event (one u32 per event, LDS [event][lane]):
-//   invocation  pid 3 | 0 | code 3 | a 3 | b 3 | 0 (5 bits) | val 14 (signed)
+//   invocation  pid 3 | 0 | code 3 | a 3 | 0 (5 bits) | b 3 | val 14 (signed)
 //   response    pid 3 | 1 | code 3 | val 25 (signed)
 // Staging writes a marker instead of an event it cannot hold: an invocation
 // with code 7 (not an encodable event: ENCODE_ERROR) or code 6 (a value
-// outside the ranges above: the history goes to the next stage).
+// outside the ranges above: the history goes to the next stage), or code 6
+// with bit 7 set (an event with a field of 8 or more -- an encode error, or
+// a legal event with junk in a field its constructor does not use -- that
+// finish_lane classifies from the raw event: ENCODE_ERROR or the next stage).
 constexpr int32_t IVAL_BITS = 14, RVAL_BITS = 25;
-constexpr uint32_t MARK_BAD = 0x70u, MARK_WIDE = 0x60u;
+constexpr uint32_t MARK_BAD = 0x70u, MARK_WIDE = 0x60u, MARK_SUSP = 0xE0u;
+// the legal (resp, code) pairs of a model, bit resp | code << 1: Bank
+// invocations 0..4 and every response code 0..7, Ticket 0..1 both
+template <uint32_t MODEL>
+constexpr uint32_t kCodeOk = MODEL == QSMD_MODEL_TICKET ? 0xFu : 0xABFFu;
 // Geometry of a compact stage: <= 32 events (u32 event masks, 16 levels,
 // invocation values 14 bits, stack entries j 5 bits) or <= 64 events (u64,
 // 32 levels, 13 bits, j 6 bits).  Response words are the same.
@@ -45,7 +52,7 @@ struct G64 {
 
 __device__ __forceinline__ uint32_t c_code(uint32_t w) { return (w >> 4) & 7u; }
 __device__ __forceinline__ uint32_t c_a(uint32_t w) { return (w >> 7) & 7u; }
-__device__ __forceinline__ uint32_t c_b(uint32_t w) { return (w >> 10) & 7u; }
+__device__ __forceinline__ uint32_t c_b(uint32_t w) { return (w >> 15) & 7u; }
 template <class G = G32>
 __device__ __forceinline__ int32_t c_ival(uint32_t w) { return (int32_t)w >> (32 - G::IVB); }
 __device__ __forceinline__ int32_t c_rval(uint32_t w) { return (int32_t)w >> (32 - RVAL_BITS); }
@@ -148,17 +155,23 @@ __device__ __forceinline__ bool valid_bits(uint32_t lo) {
     }
 }
 
-// The compressed word of one event, or a marker (MARK_BAD / MARK_WIDE).
-// A value fits when the word's value field sign-extends back to it.
+// The compressed word of one event, or a marker.  For a `plain` event --
+// pid, code, a and b each below 8, the only events encoders write -- the
+// fields come from two shifted copies of the lo word (lo >> 4: resp and
+// code beside the pid; lo >> 9: a and b), and a legal code is one table
+// bit; anything else is MARK_SUSP (classified by finish_lane).  A value
+// fits when the word's value field sign-extends back to it.
 template <uint32_t MODEL, class G = G32>
 __device__ __forceinline__ uint32_t compress(uint32_t lo, int32_t val) {
+    const uint32_t t = (lo & 7u) | ((lo >> 4) & ~7u);                 // pid | resp << 3 | code << 4 | ...
+    const uint32_t head = (t & 0x7Fu) | ((lo >> 9) & ~0x7Fu);         // ... | a << 7 | b << 15
     const bool resp = (lo & 0x80u) != 0u;
-    const uint32_t head = (lo & 7u) | ((lo >> 4) & 0x78u);                      // pid | resp | code
-    const uint32_t inv = head | ((lo >> 9) & 0x380u) | ((lo >> 14) & 0x1C00u) | ((uint32_t)val << (32 - G::IVB));
-    const uint32_t rsp = head | ((uint32_t)val << (32 - RVAL_BITS));
+    const uint32_t inv = head | ((uint32_t)val << (32 - G::IVB));
+    const uint32_t rsp = (head & 0x7Fu) | ((uint32_t)val << (32 - RVAL_BITS));
     const uint32_t w = resp ? rsp : inv;
     const bool fit = ((int32_t)w >> (resp ? 32 - RVAL_BITS : 32 - G::IVB)) == val;
-    return !valid_bits<MODEL>(lo) ? MARK_BAD : (fit ? w : MARK_WIDE);
+    const bool plain = (lo & 0xF8F8F878u) == 0u && ((kCodeOk<MODEL> >> ((t >> 3) & 15u)) & 1u);
+    return plain ? (fit ? w : MARK_WIDE) : MARK_SUSP;
 }
 
 // The DFS stack: LEVELS entries x 8 bits in NW VGPRs, kept as a shift
@@ -327,17 +340,17 @@ __device__ __forceinline__ void stage_packed(const SearchArgs& a, uint32_t N0, u
     else stage_packed_body<MODEL, G, false>(a, N0, off0, nh, s_ev, lane);
 }
 
-// Per lane, over its own column: the encoding checks (markers, pid <
-// n_pid) and the register masks (RESP / INV, the pid bit slices), 8 events
+// Per lane, over its own column (evp: its raw events, read only for a
+// MARK_SUSP): the encoding checks (markers, pid < n_pid) and the register masks (RESP / INV, the pid bit slices), 8 events
 // at a time with the event index wave-uniform (the calling lanes' longest
 // history bounds the loop: no indexed registers, no per-event branches).
 // No pairing: the compact stages search every history on the general path
 // (pid masks), which costs less per DFS step than pairing the invocations
 // at staging costs per event (A/B in flight, config 2: 6.44e9 vs 6.10e9
 // histories/s).  Words beyond n_ev (stale) are masked out by ALL.
-template <class G = G32>
+template <uint32_t MODEL, class G = G32>
 __device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane, uint32_t n_ev, uint32_t n_pid,
-                                            StagedT<typename G::M>& s) {
+                                            const uint2* evp, StagedT<typename G::M>& s) {
     using M = typename G::M;
     constexpr uint32_t U = 8;
     // a ballot max: the callers may be a subset of the wavefront
@@ -366,13 +379,20 @@ __device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane,
         uint32_t W[U];
 #pragma unroll
         for (uint32_t k = 0; k < U; ++k) W[k] = s_ev[c0 + k][lane];
-        uint32_t nib = 0u, mk = 0u;
-#pragma unroll
-        for (uint32_t k = 0; k < U; ++k) {
-            const uint32_t w = W[k];
-            nib |= (w & 0xFu) << (4u * k);
-            mk |= ((w & (w << 1) & ~(w << 3)) >> 6 & 1u) << k;
-        }
+        // the low bytes of the even / odd events, four to a word (v_perm;
+        // selector 0x0C = a zero byte): x0 = [w0, w2, w4, w6], x1 = [w1, w3, w5, w7]
+        const uint32_t x0 = __builtin_amdgcn_perm(W[2], W[0], 0x0C0C0400u) |
+                            __builtin_amdgcn_perm(W[6], W[4], 0x04000C0Cu);
+        const uint32_t x1 = __builtin_amdgcn_perm(W[3], W[1], 0x0C0C0400u) |
+                            __builtin_amdgcn_perm(W[7], W[5], 0x04000C0Cu);
+        const uint32_t nib = (x0 & 0x0F0F0F0Fu) | ((x1 & 0x0F0F0F0Fu) << 4);    // event k at bits 4k..4k+3
+        // marker bytes (bits 5, 6 set, 3 clear) at bit 6 of each byte, then
+        // one bit per event: m has events 0, 1 at bits 0, 1, 2, 3 at 8, 9, ...
+        const uint32_t y0 = x0 & (x0 << 1) & ~(x0 << 3) & 0x40404040u;
+        const uint32_t y1 = x1 & (x1 << 1) & ~(x1 << 3) & 0x40404040u;
+        const uint32_t m = (y0 >> 6) | (y1 >> 5);
+        const uint32_t z = m | (m >> 6);                                         // events 0-3 at 0-3, 4-7 at 16-19
+        const uint32_t mk = (z & 0xFu) | ((z >> 12) & 0xF0u);
         RESP |= (M)plane8(nib, 3) << c0;
         P0 |= (M)plane8(nib, 0) << c0;
         P1 |= (M)plane8(nib, 1) << c0;
@@ -383,7 +403,9 @@ __device__ __forceinline__ void finish_lane(uint32_t (*s_ev)[C_LANES], int lane,
     if (__ballot((MK & ALL) != (M)0)) {
 #pragma unroll 1
         for (uint32_t e = 0; e < n_max; ++e) {
-            const uint32_t mkw = s_ev[e][lane] & 0x78u;
+            uint32_t mkw = s_ev[e][lane] & 0xF8u;
+            // (a MARK_SUSP event: illegal => ENCODE_ERROR, legal => the next stage)
+            if (mkw == MARK_SUSP && e < n_ev) mkw = valid_bits<MODEL>(evp[e].x) ? MARK_WIDE : MARK_BAD;
             BAD |= (M)(mkw == MARK_BAD ? 1u : 0u) << e;
             WIDE |= (M)(mkw == MARK_WIDE ? 1u : 0u) << e;
         }
@@ -431,10 +453,20 @@ struct LaneDFS {
     uint64_t nodes;
     StackN<G::LEVELS / 4> stk;
 
-    // events whose pid equals the pid of event j (bit-sliced compare)
+    // events whose pid equals the pid of event j (bit-sliced compare); the
+    // bits beyond the history are not cleared -- every use ANDs the result
+    // with INV or RESP (u32: each slice's bit j sign-extended by one v_bfe_i32,
+    // then two 3-input logic ops)
     __device__ __forceinline__ M same_pid(uint32_t j) const {
-        const M m0 = (M)0 - ((P0 >> j) & (M)1), m1 = (M)0 - ((P1 >> j) & (M)1), m2 = (M)0 - ((P2 >> j) & (M)1);
-        return ~((P0 ^ m0) | (P1 ^ m1) | (P2 ^ m2)) & ALL;
+        if constexpr (sizeof(M) == 4) {
+            const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int32_t)P0, j, 1u);
+            const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int32_t)P1, j, 1u);
+            const uint32_t m2 = (uint32_t)__builtin_amdgcn_sbfe((int32_t)P2, j, 1u);
+            return ~((P0 ^ m0) | (P1 ^ m1) | (P2 ^ m2));
+        } else {
+            const M m0 = (M)0 - ((P0 >> j) & (M)1), m1 = (M)0 - ((P1 >> j) & (M)1), m2 = (M)0 - ((P2 >> j) & (M)1);
+            return ~((P0 ^ m0) | (P1 ^ m1) | (P2 ^ m2));
+        }
     }
 
     __device__ __forceinline__ void init(const StagedT<M>& s, const SearchArgs& a, int32_t (*s_bal)[C_LANES],
@@ -643,6 +675,36 @@ struct Counters {
                          : lane == T_ERR     ? t_err
                          : lane == T_ENC     ? t_enc
                          : lane == T_BUDGET  ? t_bud
+                         : lane == T_NODES   ? t_nodes
+                                             : 0ull;
+        bucket_add(buckets, blockIdx.x, (uint32_t)lane, v);
+    }
+};
+
+// The same totals for a wavefront whose lanes all reach the count together
+// (the compact stages): the status counts as ballots into wave-uniform
+// scalars, only the node count summed over the lanes at the flush (one
+// reduction instead of six).
+struct WaveCounters {
+    uint32_t lin = 0, nonlin = 0, err = 0, enc = 0, budget = 0;
+    uint64_t nodes = 0;
+    // out: this lane's history is final here (SKIPPED: counted by early_exit_fixup)
+    __device__ __forceinline__ void add(bool out, int status, uint64_t n) {
+        lin += (uint32_t)__builtin_popcountll(__ballot(out && status == QSMD_STATUS_LINEARISABLE));
+        nonlin += (uint32_t)__builtin_popcountll(__ballot(out && status == QSMD_STATUS_NONLINEARISABLE));
+        err += (uint32_t)__builtin_popcountll(__ballot(out && status == QSMD_STATUS_MODEL_ERROR));
+        enc += (uint32_t)__builtin_popcountll(__ballot(out && status == QSMD_STATUS_ENCODE_ERROR));
+        budget += (uint32_t)__builtin_popcountll(__ballot(out && status == QSMD_STATUS_BUDGET));
+        nodes += (out && status != QSMD_STATUS_SKIPPED) ? n : 0ull;
+    }
+    __device__ __forceinline__ void flush(unsigned long long* buckets, int lane) const {
+        const uint64_t t_nodes = wave_sum64(nodes);
+        const uint64_t v = lane == T_CHECKED ? (uint64_t)lin + nonlin + err
+                         : lane == T_LIN     ? lin
+                         : lane == T_NONLIN  ? nonlin
+                         : lane == T_ERR     ? err
+                         : lane == T_ENC     ? enc
+                         : lane == T_BUDGET  ? budget
                          : lane == T_NODES   ? t_nodes
                                              : 0ull;
         bucket_add(buckets, blockIdx.x, (uint32_t)lane, v);

@@ -246,7 +246,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
     StagedT<M> s{0, 0, 0, 0, 0, true, true};
     if (active) {
         stage_lane<MODEL, G>(a, H, L.ev, lane);
-        finish_lane<G>(L.ev, lane, H.n_ev, H.n_pid, s);
+        finish_lane<MODEL, G>(L.ev, lane, H.n_ev, H.n_pid, a.events + H.ev_off, s);
     }
     if constexpr (ST) {
         c0 = __builtin_amdgcn_s_memtime();

@@ -852,6 +852,12 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
                                                                    : QSMD_STATUS_NONLINEARISABLE);
 }
 
+__device__ __forceinline__ void clear_table(uint32_t* tab, uint32_t buckets, int lane) {
+    // every word 0xFFFFFFFF (word 2 never matches), 16 B per lane and store
+    uint4* t4 = reinterpret_cast<uint4*>(tab);
+    for (uint32_t k = (uint32_t)lane; k < buckets * 16u; k += 64u) t4[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
+}
+
 // One history h (its header H) searched by the whole wavefront (wide: from
 // stage 0w's deferred list).
 template <uint32_t MODEL, typename M>
@@ -960,6 +966,12 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
             return;
         }
     }
+    if (status < 0 && dag_base) {
+        // the DAG did not fit and its arrays share the LDS with the memo
+        // table (wave_lds: one region, the larger of the two): clear it
+        clear_table(tab, p.buckets, lane);
+        __syncthreads();
+    }
     bool skip = false;
     uint32_t iter = 0;
     const uint32_t min_rem = p.memo_min_rem;
@@ -1045,12 +1057,6 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
     }
 }
 
-__device__ __forceinline__ void clear_table(uint32_t* tab, uint32_t buckets, int lane) {
-    // every word 0xFFFFFFFF (word 2 never matches), 16 B per lane and store
-    uint4* t4 = reinterpret_cast<uint4*>(tab);
-    for (uint32_t k = (uint32_t)lane; k < buckets * 16u; k += 64u) t4[k] = make_uint4(~0u, ~0u, ~0u, ~0u);
-}
-
 }  // namespace
 
 // The three lists (stage 0's heavy, stage 0w's heavy, stage 0w's wide), one
@@ -1070,7 +1076,7 @@ __global__ __launch_bounds__(C_LANES) void wave_search(WaveArgs p) {
     const uint32_t nw = p.list_wide ? *p.count_wide : (uint32_t)p.s.n_hist;
     const uint64_t t0 = p.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     Counters cnt;
-    uint32_t* dag = p.dag_states ? tab + p.buckets * 64u : nullptr;
+    uint32_t* dag = p.dag_states ? tab : nullptr;   // (the DAG arrays over the memo table: wave_lds)
     clear_table(tab, p.buckets, lane);
     uint32_t epoch = 0u, victim = 0u;
     for (uint32_t i = blockIdx.x; i < n32 + n64 + nw; i += gridDim.x) {
@@ -1111,10 +1117,16 @@ __global__ __launch_bounds__(C_LANES) void wave_search(WaveArgs p) {
     cnt.flush(p.s.buckets, lane);
 }
 
-// dynamic LDS of one workgroup: the memo table, then the DAG arrays
+// dynamic LDS of one workgroup: the memo table and the DAG arrays in one
+// region (a history runs the DFS, with the memo, only when its DAG did not
+// fit, and the table is cleared then), so a config-2 call's ~2300 heavy
+// histories are resident at once (16 workgroups per CU; with the two regions
+// side by side, 9 per CU: two rounds)
 template <uint32_t MODEL, typename M>
 static size_t wave_lds(const WaveArgs& p) {
-    return (size_t)p.buckets * 64u * 4u + (p.dag_states ? dag_lds_bytes<MODEL, M>(p.dag_states, p.dag_items) : 0u);
+    const size_t memo = (size_t)p.buckets * 64u * 4u;
+    const size_t dag = p.dag_states ? dag_lds_bytes<MODEL, M>(p.dag_states, p.dag_items) : 0u;
+    return memo > dag ? memo : dag;
 }
 
 constexpr size_t kMaxLds = 160u * 1024u;   // gfx950: LDS per workgroup at most

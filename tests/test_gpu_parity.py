@@ -562,6 +562,54 @@ def test_device_resident_full_size(ctx, name, n):
         assert (st == codec.STATUS_NONLIN).sum() > n // 10   # the early-termination path is exercised
 
 
+@pytest.mark.parametrize("name,n", [("bank_4x16", 1_000_000), ("bank_4x16_bugs", 1_250_000)])
+def test_bench_knobs_in_flight_full_size(name, n):
+    """bench.py's own knob set at full size: stage-0 budget 26, the heavy
+    stage in lane mode with HBM memo tables (heavy_mode 1, memo_lds 0), three
+    contexts on three streams with calls in flight (each context's second
+    call sizes its tail grids and lane tables from its first), on config 2
+    (1M) and on config 3's per-GPU share of 10M over 8 GPUs (1.25M): every
+    status and node count of every call equals the oracle's
+    (/root/reference/test/Bank.hs:256-287 checks one history per call)."""
+    torch = pytest.importorskip("torch")
+    mid = gen.CONFIGS[name]["model_id"]
+    hdr, ev, _ = gen.generate_config(name, 0, n)
+    dev = torch.device("cuda:0")
+    d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
+    d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
+    ctxs = [device.Context(0, time_limit_ms=60000) for _ in range(3)]
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev),
+             torch.zeros(8, dtype=torch.int64, device=dev)) for _ in range(3)]
+    try:
+        for c in ctxs:
+            c.set_stage0_budget(26)
+            c.set_param("heavy_mode", 1)
+            c.set_param("memo_lds", 0)
+        results = []
+        for rnd in range(2):
+            for i in range(3):
+                d_st, d_nd, d_tot = outs[i]
+                with torch.cuda.stream(streams[i]):
+                    d_st.fill_(0xEE)
+                    ctxs[i].check_device(mid, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st.data_ptr(),
+                                         d_nd.data_ptr(), None, d_tot.data_ptr(), flags=device.QSMD_FLAG_EXHAUSTIVE,
+                                         stream=streams[i].cuda_stream)
+            torch.cuda.synchronize()
+            results += [(o[0].cpu().numpy(), o[1].cpu().numpy().astype(np.uint64), o[2].cpu().numpy())
+                        for o in outs]
+    finally:
+        for c in ctxs:
+            c.close()
+    st_o, nd_o, _ = oracle_c.check_batch(mid, hdr, ev, threads=16)
+    for st, nd, tot in results:
+        bad = np.nonzero((st != st_o) | (nd != nd_o))[0]
+        assert len(bad) == 0, f"{len(bad)} mismatches, first {bad[:5]}"
+        assert int(tot[0]) == int((st <= 2).sum()) and int(tot[7]) == int(nd.sum())
+    if name == "bank_4x16":
+        assert (st_o == codec.STATUS_LIN).all()
+
+
 @pytest.mark.parametrize("packed", [True, False])
 def test_value_ranges_and_pairing(ctx, packed):
     """Stage 0 holds invocation values within 14-bit signed and response

@@ -5,12 +5,13 @@
 # and GPU_MAX_HW_QUEUES.  tools/gpu/rccl_sweep.sh [rounds] "TAG|ENV|ARGS" ...
 set -o pipefail
 R=${1:-3}; shift
+STEPS=${STEPS:-60}
 mkdir -p gpurun_out/rccl
 rm -f gpurun_out/rccl/*.json gpurun_out/rccl/*.err
 for spec in "$@"; do
   IFS='|' read -r tag envs args <<< "$spec"
   for r in $(seq 1 "$R"); do
-    env $envs timeout -k 10 150 python bench.py --steps 60 --warmup 5 --no-cpu-baseline --no-extra $args \
+    env $envs timeout -k 10 150 python bench.py --steps $STEPS --warmup 5 --no-cpu-baseline --no-extra $args \
         > "gpurun_out/rccl/$tag.$r.json" 2> "gpurun_out/rccl/$tag.$r.err" || exit $?
   done
 done
