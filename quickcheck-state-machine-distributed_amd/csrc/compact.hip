@@ -56,20 +56,20 @@ template <class DFS>
 __device__ __forceinline__ int run_search(DFS& dfs, const SearchArgs& a, const uint32_t* evc,
                                           int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t h,
                                           uint64_t t0) {
-    int status;
-    uint32_t iter = 0;
-    do {                                 // one exit (see LaneDFS::step)
-        status = dfs.template step<C_LANES>(a, evc, s_bal, lane, limit);
-        ++iter;
-        if ((iter & 1023u) == 0u && status < 0) {
-            if (beyond_first_fail(a, h)) {
-                status = QSMD_STATUS_SKIPPED;
-            } else if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
-                atomicOr(a.timed_out, 1u);
-                status = QSMD_STATUS_BUDGET;
-            }
+    int status = -1;
+    while (true) {
+        // 1024 steps between the checks (the inner loop's only test is the
+        // step's one exit, see LaneDFS::step)
+        for (uint32_t k = 0; k < 1024u && status < 0; ++k) status = dfs.template step<C_LANES>(a, evc, s_bal, lane, limit);
+        if (status >= 0) break;
+        if (beyond_first_fail(a, h)) {
+            status = QSMD_STATUS_SKIPPED;
+        } else if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
+            atomicOr(a.timed_out, 1u);
+            status = QSMD_STATUS_BUDGET;
         }
-    } while (status < 0);
+        if (status >= 0) break;
+    }
     return status;
 }
 
