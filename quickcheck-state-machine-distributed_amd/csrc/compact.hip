@@ -60,7 +60,12 @@ __device__ __forceinline__ int run_search(DFS& dfs, const SearchArgs& a, const u
     while (true) {
         // 1024 steps between the checks (the inner loop's only test is the
         // step's one exit, see LaneDFS::step)
-        for (uint32_t k = 0; k < 1024u && status < 0; ++k) status = dfs.template step<C_LANES>(a, evc, s_bal, lane, limit);
+        // (a wavefront-uniform counter: the loop runs while any lane
+        // searches, the finished lanes masked off)
+        for (uint32_t k = 0; k < 1024u; ++k) {
+            if (status < 0) status = dfs.template step<C_LANES>(a, evc, s_bal, lane, limit);
+            if (__ballot(status < 0) == 0ull) break;
+        }
         if (status >= 0) break;
         if (beyond_first_fail(a, h)) {
             status = QSMD_STATUS_SKIPPED;
@@ -70,7 +75,7 @@ __device__ __forceinline__ int run_search(DFS& dfs, const SearchArgs& a, const u
         }
         if (status >= 0) break;
     }
-    return status;
+    return dfs.finish(status);
 }
 
 #if QSMD_DIAG_STAGE0 == 2
@@ -83,7 +88,7 @@ __device__ __forceinline__ int run_search_counted(DFS& dfs, const SearchArgs& a,
         status = dfs.template step<C_LANES>(a, evc, s_bal, lane, limit);
         ++iter;
     } while (status < 0);
-    return status;
+    return dfs.finish(status);
 }
 #endif
 

@@ -24,35 +24,38 @@ constexpr int C_CHUNK = 16;
 constexpr int32_t V19_MIN = -(1 << 18), V19_MAX = (1 << 18) - 1;   // model0 values (api.hip m0_small)
 
 // compressed event (one u32 per event, LDS [event][lane]):
-//   invocation  pid 3 | 0 | code 3 | a 3 | 0 (5 bits) | b 3 | val 14 (signed)
+//   invocation  pid 3 | 0 | code 3 | 0 (5 bits) | a 3 | 0 (5) | b 3 | val 9 (signed)
 //   response    pid 3 | 1 | code 3 | val 25 (signed)
+// (the invocation's fields where lo >> 4 puts them; Bank money in the
+// reference comes from QuickCheck's getPositive at sizes <= 100,
+// test/Bank.hs:139-144)
 // Staging writes a marker instead of an event it cannot hold: an invocation
 // with code 7 (not an encodable event: ENCODE_ERROR) or code 6 (a value
 // outside the ranges above: the history goes to the next stage), or code 6
 // with bit 7 set (an event with a field of 8 or more -- an encode error, or
 // a legal event with junk in a field its constructor does not use -- that
 // finish_lane classifies from the raw event: ENCODE_ERROR or the next stage).
-constexpr int32_t IVAL_BITS = 14, RVAL_BITS = 25;
+constexpr int32_t IVAL_BITS = 9, RVAL_BITS = 25;
 constexpr uint32_t MARK_BAD = 0x70u, MARK_WIDE = 0x60u, MARK_SUSP = 0xE0u;
-// the legal (resp, code) pairs of a model, bit resp | code << 1: Bank
-// invocations 0..4 and every response code 0..7, Ticket 0..1 both
+// the illegal (resp, code) pairs of a model, bit resp | code << 1: Bank
+// invocations 0..4 and every response code 0..7 are legal, Ticket 0..1 both
 template <uint32_t MODEL>
-constexpr uint32_t kCodeOk = MODEL == QSMD_MODEL_TICKET ? 0xFu : 0xABFFu;
+constexpr uint32_t kCodeBad = (MODEL == QSMD_MODEL_TICKET ? 0xFu : 0xABFFu) ^ 0xFFFFu;
 // Geometry of a compact stage: <= 32 events (u32 event masks, 16 levels,
-// invocation values 14 bits, stack entries j 5 bits) or <= 64 events (u64,
-// 32 levels, 13 bits, j 6 bits).  Response words are the same.
+// stack entries j 5 bits) or <= 64 events (u64, 32 levels, j 6 bits).  The
+// event words are the same.
 struct G32 {
     using M = uint32_t;
-    static constexpr int EV = 32, RB = 5, IVB = 14, LEVELS = 16;
+    static constexpr int EV = 32, RB = 5, IVB = IVAL_BITS, LEVELS = 16;
 };
 struct G64 {
     using M = uint64_t;
-    static constexpr int EV = 64, RB = 6, IVB = 13, LEVELS = 32;
+    static constexpr int EV = 64, RB = 6, IVB = IVAL_BITS, LEVELS = 32;
 };
 
 __device__ __forceinline__ uint32_t c_code(uint32_t w) { return (w >> 4) & 7u; }
-__device__ __forceinline__ uint32_t c_a(uint32_t w) { return (w >> 7) & 7u; }
-__device__ __forceinline__ uint32_t c_b(uint32_t w) { return (w >> 15) & 7u; }
+__device__ __forceinline__ uint32_t c_a(uint32_t w) { return (w >> 12) & 7u; }
+__device__ __forceinline__ uint32_t c_b(uint32_t w) { return (w >> 20) & 7u; }
 template <class G = G32>
 __device__ __forceinline__ int32_t c_ival(uint32_t w) { return (int32_t)w >> (32 - G::IVB); }
 __device__ __forceinline__ int32_t c_rval(uint32_t w) { return (int32_t)w >> (32 - RVAL_BITS); }
@@ -66,6 +69,9 @@ __device__ __forceinline__ uint32_t m_ctz(uint32_t x) { return (uint32_t)__built
 __device__ __forceinline__ uint32_t m_ctz(uint64_t x) { return (uint32_t)__builtin_ctzll(x); }
 __device__ __forceinline__ uint32_t m_hibit(uint32_t x) { return 31u - (uint32_t)__builtin_clz(x); }
 __device__ __forceinline__ uint32_t m_hibit(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
+// the highest set bit of x != 0 as a mask (v_ffbh + one shift)
+__device__ __forceinline__ uint32_t m_topbit(uint32_t x) { return 0x80000000u >> __builtin_clz(x); }
+__device__ __forceinline__ uint64_t m_topbit(uint64_t x) { return 0x8000000000000000ull >> __builtin_clzll(x); }
 
 // candidates: remaining invocations before the first remaining response
 // (takeInvocations, src/Linearisability.hs:25-28); branch-free
@@ -157,20 +163,19 @@ __device__ __forceinline__ bool valid_bits(uint32_t lo) {
 
 // The compressed word of one event, or a marker.  For a `plain` event --
 // pid, code, a and b each below 8, the only events encoders write -- the
-// fields come from two shifted copies of the lo word (lo >> 4: resp and
-// code beside the pid; lo >> 9: a and b), and a legal code is one table
+// invocation is lo >> 4 with the pid put back in its low bits and the value
+// above, the response keeps the low 7 bits, and a legal code is one table
 // bit; anything else is MARK_SUSP (classified by finish_lane).  A value
 // fits when the word's value field sign-extends back to it.
 template <uint32_t MODEL, class G = G32>
 __device__ __forceinline__ uint32_t compress(uint32_t lo, int32_t val) {
-    const uint32_t t = (lo & 7u) | ((lo >> 4) & ~7u);                 // pid | resp << 3 | code << 4 | ...
-    const uint32_t head = (t & 0x7Fu) | ((lo >> 9) & ~0x7Fu);         // ... | a << 7 | b << 15
+    const uint32_t t = (lo & 7u) | ((lo >> 4) & ~7u);                 // pid | resp << 3 | code << 4 | a << 12 | b << 20
     const bool resp = (lo & 0x80u) != 0u;
-    const uint32_t inv = head | ((uint32_t)val << (32 - G::IVB));
-    const uint32_t rsp = (head & 0x7Fu) | ((uint32_t)val << (32 - RVAL_BITS));
+    const uint32_t inv = t | ((uint32_t)val << (32 - G::IVB));
+    const uint32_t rsp = (t & 0x7Fu) | ((uint32_t)val << (32 - RVAL_BITS));
     const uint32_t w = resp ? rsp : inv;
     const bool fit = ((int32_t)w >> (resp ? 32 - RVAL_BITS : 32 - G::IVB)) == val;
-    const bool plain = (lo & 0xF8F8F878u) == 0u && ((kCodeOk<MODEL> >> ((t >> 3) & 15u)) & 1u);
+    const bool plain = ((lo & 0xF8F8F878u) | ((kCodeBad<MODEL> >> ((lo >> 7) & 15u)) & 1u)) == 0u;
     return plain ? (fit ? w : MARK_WIDE) : MARK_SUSP;
 }
 
@@ -280,6 +285,8 @@ __device__ __forceinline__ void stage_packed_body(const SearchArgs& a, uint32_t 
     if (((off0 | total_ev) & 1u) == 0u) {         // 16-B aligned start, whole 16-B pairs
         const uint4* blk = reinterpret_cast<const uint4*>(a.events + off0);
         const uint32_t nq = total_ev / 2u;
+        const uint32_t e_lane = POW2 ? (2u * (uint32_t)lane) & (N0 - 1u) : 0u;
+        const uint32_t c_lane = POW2 ? (2u * (uint32_t)lane) >> sh : 0u;
         // U x 64 pairs per step: full steps without per-element guards, then the rest
         auto step = [&](uint32_t k0, auto guard) {
             constexpr bool GUARD = decltype(guard)::value;
@@ -292,12 +299,20 @@ __device__ __forceinline__ void stage_packed_body(const SearchArgs& a, uint32_t 
 #pragma unroll
             for (uint32_t u = 0; u < U; ++u) {
                 const uint32_t q = k0 + u * 64u + (uint32_t)lane;
-                uint32_t e0, e1;
-                const uint32_t c0 = col_of(2u * q, e0);
-                // an even power-of-two length: both events of the pair in one
-                // history (one ds_write2 per pair)
-                const uint32_t c1 = POW2 ? c0 : col_of(2u * q + 1u, e1);
-                if (POW2) e1 = e0 + 1u;
+                uint32_t e0, e1, c0, c1;
+                if constexpr (POW2) {
+                    // an even power-of-two length N0 <= 64: both events of the
+                    // pair in one history (one ds_write2 per pair), the event
+                    // index the lane's own constant (2 (k0 + 64 u) is a multiple
+                    // of N0) and the column a wave-uniform part plus the lane's
+                    e0 = e_lane;
+                    e1 = e_lane + 1u;
+                    c0 = ((2u * (k0 + u * 64u)) >> sh) + c_lane;
+                    c1 = c0;
+                } else {
+                    c0 = col_of(2u * q, e0);
+                    c1 = col_of(2u * q + 1u, e1);
+                }
                 if (!GUARD || q < nq) {
                     s_ev[e0][c0] = compress<MODEL, G>(x[u].x, (int32_t)x[u].y);
                     s_ev[e1][c1] = compress<MODEL, G>(x[u].z, (int32_t)x[u].w);
@@ -447,7 +462,8 @@ struct LaneDFS {
     static constexpr uint32_t JB = (uint32_t)G::RB;        // stack entry: j | ex_a << JB | ex_b << JB+1
     M INV, RESP, P0, P1, P2, ALL;
     M rem, cand;
-    uint32_t depth, ex, neg, RS, found;
+    uint32_t depth, ex, RS, found;
+    int32_t neg;            // < 0: some existing balance is negative (the invariant fails)
     uint32_t base;          // depth of the search root (0; the task depth in split_search)
     uint32_t last_j;        // candidate of the most recent try (the one a BUDGET return did not count)
     uint64_t nodes;
@@ -485,7 +501,7 @@ struct LaneDFS {
                 const bool e = (ex >> q) & 1u;
                 const int32_t v = e ? (int32_t)a.m0_val[q] : 0;
                 s_bal[q][lane] = v;
-                neg |= (e && v < 0) ? (1u << q) : 0u;
+                neg |= (e && v < 0) ? v : 0;
             }
         }
     }
@@ -502,32 +518,45 @@ struct LaneDFS {
         const uint32_t j = st & JM;
         const uint32_t cj = BANK ? evc[j * STRIDE] : 0u;
         const M gone = ~rem & same_pid(j);
-        rem |= ((M)1 << m_hibit(gone & INV)) | ((M)1 << m_hibit(gone & RESP));
+        rem |= m_topbit(gone & INV) | m_topbit(gone & RESP);
         if constexpr (BANK) {
             const uint32_t code = c_code(cj), ia = c_a(cj), ib = c_b(cj);
             const int32_t m = c_ival<G>(cj);
-            const uint32_t pa = (st >> JB) & 1u, pb = (st >> (JB + 1u)) & 1u;
-            const uint32_t tr = code == QSMD_BANK_TRANSFER ? 1u : 0u;
+            // -(exists a), -(exists b) before the step (the stack entry's bits)
+            const int32_t pam = __builtin_amdgcn_sbfe((int32_t)st, JB, 1u);
+            const int32_t pbm = __builtin_amdgcn_sbfe((int32_t)st, JB + 1u, 1u);
+            const bool tr = code == QSMD_BANK_TRANSFER, same = ia == ib;
             int32_t ba = s_bal[ia][lane], bb = s_bal[ib][lane];
             // both reads in flight together: without this the compiler sinks
             // ba's read into a branch on the pre-op `exists a` bit, a second
             // serial LDS round trip per backtrack
             asm volatile("" : "+v"(ba), "+v"(bb));
             // undo Transfer's deposit on b, then the step on a
-            const int32_t rb = (pb | (ia == ib)) ? bb - m : 0;
-            const int32_t cur_a = (tr & (ia == ib)) ? rb : ba;
-            const int32_t ra = pa ? cur_a - bank_sign(code) * m : 0;
+            const int32_t rb = (bb - m) & (pbm | (same ? -1 : 0));
+            const int32_t cur_a = (tr & same) ? rb : ba;
+            const int32_t ra = (cur_a - bank_sign(code) * m) & pam;
             const int32_t fb = tr ? rb : bb;
             s_bal[ib][lane] = fb;                  // a no-op unless Transfer
             s_bal[ia][lane] = ra;                  // written last (ia == ib)
-            ex = (ex & ~((1u << ia) | (tr << ib))) | (pa << ia) | ((tr & pb) << ib);
+            // the existence bits of a (and b for Transfer) back to the stack's
+            const uint32_t A = 1u << ia, B = tr ? 1u << ib : 0u;
+            ex = (ex & ~A) | (A & (uint32_t)pam);
+            ex = (ex & ~B) | (B & (uint32_t)pbm);
             // the parent held the invariant (a step descends only when it
             // holds, test/Bank.hs:118), so no existing balance was negative
-            neg = 0u;
+            neg = 0;
         } else {
             RS &= ~(1u << depth);
         }
         return j;
+    }
+
+    // step()'s return for a search that ended (a leaf or the exhausted
+    // root): finish() turns it into the outcome once, after the loop
+    static constexpr int kTerm = 64;
+    __device__ __forceinline__ int finish(int status) const {
+        return status != kTerm ? status
+                               : ((!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE);
     }
 
     template <int STRIDE>
@@ -539,8 +568,7 @@ struct LaneDFS {
         // a subtree rooted at depth base > 0 is an inner node of the reference tree
         const bool empty = cand == (M)0;
         const bool term = empty & ((found == 0u) | (depth == base));
-        int status = !term ? -1
-                           : ((!found && depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE);
+        int status = term ? kTerm : -1;    // (the outcome itself: finish())
         if (empty & !term) {
             // ---- backtrack: restore the parent level exactly
             const uint32_t j = undo<STRIDE>(evc, s_bal, lane);
@@ -574,15 +602,19 @@ struct LaneDFS {
         if constexpr (BANK) {
             const uint32_t ia = c_a(cj), ib = c_b(cj);
             const int32_t bal_a = s_bal[ia][lane], bal_b = s_bal[ib][lane];
-            const uint32_t ex_a = (ex >> ia) & 1u, ex_b = (ex >> ib) & 1u;
+            // exm = -(exists a): one v_bfe_i32 serves the test, the stack
+            // entry and the masked balance below
+            const int32_t exm = __builtin_amdgcn_sbfe((int32_t)ex, ia, 1u);
+            const bool ex_a = exm != 0;
+            const int32_t exbm = __builtin_amdgcn_sbfe((int32_t)ex, ib, 1u);   // -(exists b)
             // post (test/Bank.hs:118-131): invariant && expected response
             const bool tr = code == QSMD_BANK_TRANSFER;
             const bool chk = code == QSMD_BANK_CHECK_BALANCE;
             const bool same = ia == ib;
             // expected constructor: kBankExp2[code][exists a (Open) / lookup a >= Just m]
-            const uint32_t sel = ((code == QSMD_BANK_OPEN_ACCOUNT) | (bal_a >= m)) ? ex_a : 0u;
-            const uint32_t exp = __builtin_amdgcn_ubfe(kBankExp2, code * 6u + sel * 3u, 3u);
-            const bool inv_ok = neg == 0u;
+            const bool sel = ex_a & ((code == QSMD_BANK_OPEN_ACCOUNT) | (bal_a >= m));
+            const uint32_t exp = __builtin_amdgcn_ubfe(kBankExp2, code * 6u + (sel ? 3u : 0u), 3u);
+            const bool inv_ok = neg >= 0;
             err = has & inv_ok & chk & (rc == QSMD_BANK_BALANCE) & !ex_a;   // Map.! raises
             // a raising step never descends (an absent account's stored 0
             // would otherwise match `Balance 0`)
@@ -591,18 +623,21 @@ struct LaneDFS {
             // with m exactly when the step's sign is non-zero: insertWith),
             // then Transfer's deposit on b; stored unconditionally (the old
             // values when !ok)
-            stw = j | (ex_a << JB) | (ex_b << (JB + 1u));
+            stw = j | ((uint32_t)exm & (1u << JB)) | ((uint32_t)exbm & (2u << JB));
             const int32_t sa = bank_sign(code);
-            const int32_t na = (ex_a ? bal_a : 0) + (ex_a ? sa : (sa & 1)) * m;
+            const int32_t na = (bal_a & exm) + (sa & (exm | 1)) * m;
             const int32_t bo = same ? na : bal_b;
-            const int32_t fb = tr ? (((ex_b != 0u) | same) ? bo : 0) + m : bo;
+            // Transfer: b (0 when absent; the stepped a when b == a) + m
+            const int32_t fb = tr ? (same ? na : (bal_b & exbm)) + m : bo;
             s_bal[ia][lane] = ok ? na : bal_a;
             s_bal[ib][lane] = ok ? fb : bal_b;
             const int32_t va = same ? fb : na;
-            ex = ok ? (ex | ((chk ? 0u : 1u) << ia) | ((tr ? 1u : 0u) << ib)) : ex;
+            ex |= ((ok & !chk) ? 1u : 0u) << ia;
+            ex |= ((ok & tr) ? 1u : 0u) << ib;
             // ok => the invariant held before the step and absent accounts
-            // hold 0: the child breaks it iff a or b went negative
-            neg = ok ? (((va | fb) < 0) ? 1u : 0u) : neg;
+            // hold 0: the child breaks it iff a or b went negative (the sign
+            // of va | fb)
+            neg = ok ? (va | fb) : neg;
         } else {
             // model at this depth: Just (#TT since the last Reset), or model0
             // advanced by succ <$> once per level
