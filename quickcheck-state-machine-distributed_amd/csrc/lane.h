@@ -163,20 +163,25 @@ __device__ __forceinline__ bool valid_bits(uint32_t lo) {
 
 // The compressed word of one event, or a marker.  For a `plain` event --
 // pid, code, a and b each below 8, the only events encoders write -- the
-// invocation is lo >> 4 with the pid put back in its low bits and the value
-// above, the response keeps the low 7 bits, and a legal code is one table
-// bit; anything else is MARK_SUSP (classified by finish_lane).  A value
-// fits when the word's value field sign-extends back to it.
+// invocation is lo >> 4 with the pid put back in its low bits (a bit
+// insert) and the value above, the response keeps the low 7 bits, and a
+// legal code is one table bit; a value fits when the word's value field
+// sign-extends back to it.  Anything else is MARK_SUSP, classified from the
+// raw event by finish_lane (an encode error, or a legal event for the next
+// stage: junk in a field its constructor does not use, a value too wide).
 template <uint32_t MODEL, class G = G32>
 __device__ __forceinline__ uint32_t compress(uint32_t lo, int32_t val) {
-    const uint32_t t = (lo & 7u) | ((lo >> 4) & ~7u);                 // pid | resp << 3 | code << 4 | a << 12 | b << 20
-    const bool resp = (lo & 0x80u) != 0u;
-    const uint32_t inv = t | ((uint32_t)val << (32 - G::IVB));
-    const uint32_t rsp = (t & 0x7Fu) | ((uint32_t)val << (32 - RVAL_BITS));
-    const uint32_t w = resp ? rsp : inv;
-    const bool fit = ((int32_t)w >> (resp ? 32 - RVAL_BITS : 32 - G::IVB)) == val;
-    const bool plain = ((lo & 0xF8F8F878u) | ((kCodeBad<MODEL> >> ((lo >> 7) & 15u)) & 1u)) == 0u;
-    return plain ? (fit ? w : MARK_WIDE) : MARK_SUSP;
+    static_assert(32 - G::IVB == 23 && 32 - RVAL_BITS == 7, "value field shifts");
+    uint32_t t;                                                       // pid | resp << 3 | code << 4 | a << 12 | b << 20
+    asm("v_bfi_b32 %0, 7, %1, %2" : "=v"(t) : "v"(lo), "v"(lo >> 4));   // (hipcc emits and + and_or)
+    const uint32_t sh = 23u - (__builtin_amdgcn_ubfe(lo, 7u, 1u) << 4);   // response: 7
+    // a plain invocation's t is below 2^23; a response keeps pid | 1 | code
+    const uint32_t w = ((uint32_t)val << sh) | __builtin_amdgcn_ubfe(t, 0u, sh);
+    const bool fit = ((int32_t)w >> sh) == val;
+    // (resp | code << 1 | code bit 3 << 4: bit 11 is in the field mask too)
+    const uint32_t bad = __builtin_amdgcn_ubfe(kCodeBad<MODEL> | 0xFFFF0000u, __builtin_amdgcn_ubfe(lo, 7u, 5u), 1u);
+    const bool plain = ((lo & 0xF8F8F878u) | bad) == 0u;
+    return (plain & fit) ? w : MARK_SUSP;
 }
 
 // The DFS stack: LEVELS entries x 8 bits in NW VGPRs, kept as a shift
