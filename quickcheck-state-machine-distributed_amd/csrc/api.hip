@@ -189,6 +189,12 @@ void stage_done(const char* name, hipStream_t s, const uint32_t* cnt) {
     const hipError_t e = hipStreamSynchronize(s);
     uint32_t h[C_N] = {};
     (void)hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost);
+    {   // stage 0's heavy list: its shard counters (internal.h)
+        uint32_t sh[kShards * kShardStride];
+        (void)hipMemcpy(sh, reinterpret_cast<const char*>(cnt) - kOffCnt + kOffShards, sizeof sh,
+                        hipMemcpyDeviceToHost);
+        for (uint32_t k = 0; k < kShards; ++k) h[C_HEAVY32] += sh[k * kShardStride];
+    }
     const auto t = std::chrono::steady_clock::now();
     std::fprintf(stderr, "[qsmd] %-8s %s %.3f ms  defer %u heavy %u/%u giants %u timed %u tasks %u/%u\n", name,
                  hipGetErrorString(e), std::chrono::duration<double, std::milli>(t - t_prev).count(), h[C_DEFER],
@@ -509,8 +515,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const uint64_t n_tk = (uint64_t)SPLIT_VARIANTS * kTaskCap;
     const size_t lst = align_up(n_hist * 4 + 4);
     const size_t off_l0 = kWsHeader;                     // stage 0 -> stage 0w
+    const uint64_t cap32 = shard_cap(n_hist);            // stage 0's heavy list: kShards shards (internal.h)
     const size_t off_h32 = off_l0 + lst;                 // heavy lists
-    const size_t off_h64 = off_h32 + lst;
+    const size_t off_h64 = off_h32 + align_up(kShards * cap32 * 4 + 4);
     const size_t off_lw = off_h64 + lst;                 // stage 0w's deferred (wide) histories
     const size_t off_lg = off_lw + lst;                  // giants
     const size_t off_gr = off_lg + lst;
@@ -532,6 +539,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     qsmd_totals* tot = totals ? totals : reinterpret_cast<qsmd_totals*>(c->ws + off_tot);
     uint32_t* l0 = reinterpret_cast<uint32_t*>(c->ws + off_l0);
     uint32_t* h32 = reinterpret_cast<uint32_t*>(c->ws + off_h32);
+    uint32_t* shards = reinterpret_cast<uint32_t*>(c->ws + kOffShards);
     uint32_t* h64 = reinterpret_cast<uint32_t*>(c->ws + off_h64);
     uint32_t* lw = reinterpret_cast<uint32_t*>(c->ws + off_lw);
     uint32_t* lg = reinterpret_cast<uint32_t*>(c->ws + off_lg);
@@ -564,7 +572,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.defer_list = l0;
     a0.defer_count = cnt + C_DEFER;
     a0.heavy_list = h32;
-    a0.heavy_count = cnt + C_HEAVY32;
+    a0.heavy_count = shards;
+    a0.heavy_shard_cap = (uint32_t)cap32;
     a0.stage0_budget = c->stage0_budget ? c->stage0_budget : ~0ull;
     a0.stamps = c->s0_stamps;
     const uint64_t n_groups = std::max<uint64_t>((n_hist + 63) / 64, 1);
@@ -603,7 +612,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         for (int w = 0; w < 2; ++w) {
             mp[w].s = a;
             mp[w].s.list = w ? h64 : h32;
-            mp[w].s.list_count = cnt + (w ? C_HEAVY64 : C_HEAVY32);
+            mp[w].s.list_count = w ? cnt + C_HEAVY64 : shards;
+            mp[w].s.list_shard_cap = w ? 0u : (uint32_t)cap32;
             mp[w].table = reinterpret_cast<uint32_t*>(c->mt + (w ? slots * 32 : 0));
             mp[w].entries = (uint32_t)c->mt_entries;
             mp[w].lds_entries = lds_entries;
@@ -620,7 +630,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         WaveArgs wp{};
         wp.s = a;
         wp.list32 = h32;
-        wp.count32 = cnt + C_HEAVY32;
+        wp.count32 = shards;
+        wp.cap32 = (uint32_t)cap32;
         wp.list64 = h64;
         wp.count64 = cnt + C_HEAVY64;
         wp.list_wide = (route & kSkip0w) ? nullptr : lw;
@@ -654,6 +665,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     SplitArgs p{};
     p.s = a;
     p.cnt = cnt;
+    p.shards = shards;
     p.giant_list = lg;
     p.giant_count = cnt + C_GIANT;
     p.giants = reinterpret_cast<GiantRec*>(c->ws + off_gr);

@@ -47,6 +47,11 @@
 #ifndef QSMD_DIAG_SEARCH2
 #define QSMD_DIAG_SEARCH2 0
 #endif
+// QSMD_DIAG_NOHEAVY=1: no heavy-list append (the budget-stopped histories
+// are reported BUDGET), to price the append
+#ifndef QSMD_DIAG_NOHEAVY
+#define QSMD_DIAG_NOHEAVY 0
+#endif
 
 namespace qsmd {
 
@@ -210,8 +215,18 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
 #endif
         note_failure(a, h, status);
         // over the stage budget (not the caller's): searched again by the heavy stage
+#if QSMD_DIAG_NOHEAVY
+        const bool heavy = false;   // diagnostic build: budget-stopped histories are reported BUDGET (no list)
+#else
         const bool heavy = tiered && status == QSMD_STATUS_BUDGET && dfs.nodes >= limit;
-        wave_append(heavy, h, a.heavy_list, a.heavy_count, lane);
+        if (a.heavy_shard_cap) {    // (stage 0: the group's shard, internal.h)
+            const uint32_t k = (uint32_t)((base / C_LANES) % kShards);
+            wave_append(heavy, h, a.heavy_list + (uint64_t)k * a.heavy_shard_cap, a.heavy_count + k * kShardStride,
+                        lane);
+        } else {
+            wave_append(heavy, h, a.heavy_list, a.heavy_count, lane);
+        }
+#endif
         const bool out = live && !heavy;
         if (out) {
             a.status[h] = (uint8_t)status;

@@ -131,6 +131,14 @@ __device__ __forceinline__ int32_t bank_sign(uint32_t code) {
     return __builtin_amdgcn_sbfe((int32_t)kBankSign, code * 2u, 2u);
 }
 
+// (x << s) | y as one v_lshl_or_b32 (hipcc merges two of them into
+// shifts and an or3)
+__device__ __forceinline__ uint32_t lshl_or(uint32_t x, uint32_t s, uint32_t y) {
+    uint32_t d;
+    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(d) : "v"(x), "v"(s), "v"(y));
+    return d;
+}
+
 __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -637,8 +645,8 @@ struct LaneDFS {
             s_bal[ia][lane] = ok ? na : bal_a;
             s_bal[ib][lane] = ok ? fb : bal_b;
             const int32_t va = same ? fb : na;
-            ex |= ((ok & !chk) ? 1u : 0u) << ia;
-            ex |= ((ok & tr) ? 1u : 0u) << ib;
+            ex = lshl_or((ok & !chk) ? 1u : 0u, ia, ex);
+            ex = lshl_or((ok & tr) ? 1u : 0u, ib, ex);
             // ok => the invariant held before the step and absent accounts
             // hold 0: the child breaks it iff a or b went negative (the sign
             // of va | fb)

@@ -222,7 +222,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
                                            Counters& cnt, uint64_t t0, int lane, unsigned long long* q) {
     using M = typename G::M;
     const SearchArgs& a = p.s;
-    const uint64_t total = *a.list_count;
+    const uint64_t total = list_total(a.list_count, a.list_shard_cap);
     const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
     uint32_t* tab;
     uint32_t mask;
@@ -239,7 +239,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
     uint64_t r0 = 0, c0 = 0;
     uint32_t hits = 0;
     if constexpr (ST) r0 = __builtin_amdgcn_s_memrealtime();
-    const uint32_t h = active ? a.list[idx] : 0u;
+    const uint32_t h = active ? list_at(a.list, a.list_count, a.list_shard_cap, idx) : 0u;
     qsmd_hdr H;
     if (active) H = a.hdr[h];
     else H = qsmd_hdr{0, 0, 0, 0, 0, 0};
@@ -328,7 +328,8 @@ template <uint32_t MODEL, bool LT>
 __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32, MemoArgs p64, uint32_t wide) {
     extern __shared__ uint32_t lds[];
     const int lane = threadIdx.x;
-    const uint64_t n32 = (*p32.s.list_count + 63u) / 64u, n64 = (*p64.s.list_count + 63u) / 64u;
+    const uint64_t n32 = (list_total(p32.s.list_count, p32.s.list_shard_cap) + 63u) / 64u,
+                   n64 = (list_total(p64.s.list_count, p64.s.list_shard_cap) + 63u) / 64u;
     Counters cnt;
     const uint64_t t0 = p32.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     uint32_t* lcol = nullptr;
@@ -354,8 +355,9 @@ __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32,
             else memo_group<MODEL, G64, false, false>(p64, (grp - n32) * 64u, L, lcol, cnt, t0, lane, q);
         } else {
             const uint64_t idx = (grp - n32) * 64u + lane;
-            const bool in = idx < *p64.s.list_count;
-            wave_append(in, in ? p64.s.list[idx] : 0u, p64.s.giant_list, p64.s.giant_count, lane);
+            const bool in = idx < list_total(p64.s.list_count, p64.s.list_shard_cap);
+            wave_append(in, in ? list_at(p64.s.list, p64.s.list_count, p64.s.list_shard_cap, idx) : 0u,
+                        p64.s.giant_list, p64.s.giant_count, lane);
         }
     }
     cnt.flush(p32.s.buckets, lane);

@@ -850,7 +850,10 @@ __device__ __forceinline__ void finish_call(const SplitArgs& p, int lane) {
         for (int k = 0; k < T_N; ++k) t = lane == k ? v[k] : t;
         reinterpret_cast<unsigned long long*>(p.totals)[lane] = t;
     }
-    if (p.probe_host && lane <= (int)C_TIMED) p.probe_host[lane] = p.cnt[lane];
+    // (stage 0's heavy list: the sum of its shard counters)
+    const uint64_t heavy32 = wave_sum64(p.shards && lane < (int)kShards ? p.shards[lane * kShardStride] : 0u);
+    if (p.probe_host && lane <= (int)C_TIMED)
+        p.probe_host[lane] = lane == (int)C_HEAVY32 && p.shards ? (uint32_t)heavy32 : p.cnt[lane];
     if (p.probe_host && lane == kProbeWide) p.probe_host[kProbeWide] = p.cnt[C_WIDE];
     // restore: buckets (and the early-exit ones), then the counters
     for (uint32_t i = (uint32_t)lane; i < kBuckets * kBucketWords; i += 64u) {
@@ -858,6 +861,7 @@ __device__ __forceinline__ void finish_call(const SplitArgs& p, int lane) {
         if (p.early) xb[i] = 0ull;
     }
     if (lane < (int)C_N) p.cnt[lane] = lane == (int)C_FIRST_FAIL ? 0xFFFFFFFFu : 0u;
+    if (p.shards && lane < (int)kShards) p.shards[lane * kShardStride] = 0u;
 }
 
 }  // namespace

@@ -1072,7 +1072,7 @@ __global__ __launch_bounds__(C_LANES) void wave_search(WaveArgs p) {
     const int lane = threadIdx.x;
     // (list_wide null: every history of the batch is on the wide list -- the
     // host entry's routing when none fits the compact stages)
-    const uint32_t n32 = W128 ? 0u : *p.count32, n64 = W128 ? 0u : *p.count64;
+    const uint32_t n32 = W128 ? 0u : list_total(p.count32, p.cap32), n64 = W128 ? 0u : *p.count64;
     const uint32_t nw = p.list_wide ? *p.count_wide : (uint32_t)p.s.n_hist;
     const uint64_t t0 = p.s.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
     Counters cnt;
@@ -1080,7 +1080,7 @@ __global__ __launch_bounds__(C_LANES) void wave_search(WaveArgs p) {
     clear_table(tab, p.buckets, lane);
     uint32_t epoch = 0u, victim = 0u;
     for (uint32_t i = blockIdx.x; i < n32 + n64 + nw; i += gridDim.x) {
-        const uint32_t h = i < n32 ? p.list32[i]
+        const uint32_t h = i < n32 ? list_at(p.list32, p.count32, p.cap32, i)
                          : (i < n32 + n64 ? p.list64[i - n32]
                                           : (p.list_wide ? p.list_wide[i - n32 - n64] : i - n32 - n64));
         const qsmd_hdr H = p.s.hdr[h];
