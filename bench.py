@@ -169,13 +169,17 @@ class InFlight:
         t0 = time.perf_counter()
         for _ in range(steps):
             self.step()
-        self.drain()
         torch.cuda.synchronize(self.dev)
         # each rank's window runs from the common opening barrier to its own
         # GPU's end; the MAX over ranks below is the whole job's time, so the
         # closing barrier stays outside the window (inside it, its ~137 us of
-        # host gloo round trips were ~5 % of a 20-step run)
+        # host gloo round trips were ~5 % of a 20-step run).
+        # The counters' all-reduce runs once per block of S x ar_rounds steps
+        # inside the window; a last partial block is reduced after it (one
+        # collective's latency in a 20-step run was ~10 %)
         elapsed = time.perf_counter() - t0
+        self.drain()
+        torch.cuda.synchronize(self.dev)
         if self.use_dist:
             dist.barrier(group=self.host_group)
             torch.cuda.synchronize(self.dev)
@@ -339,7 +343,7 @@ def main():
                     help="rounds of in-flight steps whose counters one RCCL all-reduce carries (N > 1)")
     ap.add_argument("--device-gen", action="store_true",
                     help="generate the batch on the GPU (qsmd_gen_batch_device; same histories as the host generator)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r03", "stage0_pmc.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04", "stage0_pmc.json"),
                     help="PMC summary of the stage-0 kernel (profiles/summarize_pmc.py) for the roofline fields")
     ap.add_argument("--roof-calls", type=int, default=30,
                     help="synchronous calls after the timed region that time the dominant kernel alone")

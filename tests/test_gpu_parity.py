@@ -192,6 +192,19 @@ def test_generated_configs(ctx, knobs, name, n, budget, heavy):
         assert (st == codec.STATUS_LIN).all()
 
 
+@pytest.mark.parametrize("n", [1, 100, 64 * 16 * 3 + 17, 40000])
+@pytest.mark.parametrize("heavy,grid", [(0, 65536), (1, 65536), (1, 3), (0, 77)])
+def test_sharded_heavy_list(ctx, knobs, n, heavy, grid):
+    """Stage 0's heavy list in 16 shards (a group appends to shard group %
+    16; internal.h list_total / list_at): stage-0 budget 4 sends most
+    histories there -- one group (a single shard), two, an uneven 3 x 16
+    groups + 17 histories, 625 groups; grid-stride stage 0 (3 / 77
+    workgroups); both heavy modes read the shards back as one list."""
+    knobs(stage0_budget=4, heavy_mode=heavy, stage0_grid=grid)
+    hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 11, n)
+    _compare(ctx, gen.CONFIGS["bank_4x16_bugs"]["model_id"], hdr, ev, max_nodes=10**7)
+
+
 LANE_CASES = [("bank_4x16_bugs", 50000, 64, 0), ("bank_4x16_bugs", 20000, 8, 300), ("bank_4x16", 50000, 16, 0),
               ("ticket_2x10", 20000, 4, 0), ("bank_6x24", 20000, 16, 0), ("bank_6x24", 20000, 8, 500)]
 
@@ -564,7 +577,7 @@ def test_device_resident_full_size(ctx, name, n):
 
 @pytest.mark.parametrize("name,n", [("bank_4x16", 1_000_000), ("bank_4x16_bugs", 1_250_000)])
 def test_bench_knobs_in_flight_full_size(name, n):
-    """bench.py's own knob set at full size: stage-0 budget 26, the heavy
+    """bench.py's own knob set at full size: stage-0 budget 20, the heavy
     stage in lane mode with HBM memo tables (heavy_mode 1, memo_lds 0), three
     contexts on three streams with calls in flight (each context's second
     call sizes its tail grids and lane tables from its first), on config 2
@@ -583,7 +596,7 @@ def test_bench_knobs_in_flight_full_size(name, n):
              torch.zeros(8, dtype=torch.int64, device=dev)) for _ in range(3)]
     try:
         for c in ctxs:
-            c.set_stage0_budget(26)
+            c.set_stage0_budget(20)
             c.set_param("heavy_mode", 1)
             c.set_param("memo_lds", 0)
         results = []
