@@ -87,6 +87,7 @@ struct qsmd_ctx {
     // lane mode's tables: one per lane slot of the memo grid
     uint64_t memo_grid = 0;            // heavy stage (lane mode): workgroups at most (0 = 12 per CU); one table each
     uint64_t mt_entries = 128;
+    uint64_t memo_after = 32;          // lane mode: the memo joins a search after this many nodes
     uint32_t memo_lds_entries = 64;             // LDS tables: entries per lane (power of two, 4..64)
     uint64_t memo_lds_cap = 0;                  // diagnostic: LDS-table bytes accepted at most (0 = the device's)
     char* mt = nullptr;
@@ -346,6 +347,8 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         if (value < 4 || value > 64 || (value & (value - 1)))
             return fail(c, QSMD_ERR_ARG, "memo_lds_entries: a power of two in 4..64");
         c->memo_lds_entries = (uint32_t)value;
+    } else if (n == "memo_after") {
+        c->memo_after = value;
     } else if (n == "memo_lds_cap") {       // diagnostic: force the LDS-refused path (the HBM tables)
         c->memo_lds_cap = value;
     } else if (n == "memo_lds") {
@@ -616,6 +619,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].s.list_shard_cap = w ? 0u : (uint32_t)cap32;
             mp[w].table = reinterpret_cast<uint32_t*>(c->mt + (w ? slots * 32 : 0));
             mp[w].entries = (uint32_t)c->mt_entries;
+            mp[w].memo_after = (uint32_t)std::min<uint64_t>(c->memo_after, 0xFFFFFFFFull);
             mp[w].lds_entries = lds_entries;
             mp[w].epoch = c->mt_epoch;
             mp[w].giant_cap = cap;

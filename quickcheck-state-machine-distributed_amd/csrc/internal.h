@@ -291,6 +291,7 @@ struct MemoArgs {
     SearchArgs s;
     uint32_t* table;              // grid * 64 * entries * (8 | 16) u32
     uint32_t entries;
+    uint32_t memo_after;          // no memo probe / insert before a search has counted this many nodes
     uint32_t lds_entries;         // LDS tables (lds_tables): entries per lane, a power of two <= 64
     uint32_t epoch;               // this call's tag (24 bits)
     uint64_t giant_cap;           // > 0: a search past this many iterations goes to s.giant_list

@@ -151,8 +151,14 @@ __device__ __forceinline__ void memo_insert_lds(uint32_t* col, const MemoKey<MOD
 template <uint32_t MODEL, class G, bool LT>
 __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* evc,
                                          int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* tab,
-                                         uint32_t h, uint32_t epoch, uint32_t mask, uint32_t* entry, bool& skip) {
+                                         uint32_t h, uint32_t epoch, uint32_t mask, uint32_t* entry, bool& skip,
+                                         uint64_t memo_after) {
     using M = typename G::M;
+    // a short search runs as the plain DFS (no HBM probe per node); the memo
+    // joins once the search has counted memo_after nodes (entry counts are
+    // kept from the start, so a node entered before that is still recorded
+    // when it fails)
+    const bool memo = d.nodes >= memo_after;
     const bool empty = d.cand == (M)0;
     const bool term = empty & ((d.found == 0u) | (d.depth == d.base));
     int status = !term ? -1
@@ -160,7 +166,7 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     if (empty & !term) {
         // leaving the node at depth d.depth: its subtree was searched to the end and failed
         // (counts kept mod 2^32: exact while the running count is below 2^32)
-        if (!skip && d.nodes <= 0xFFFFFFFFull) {
+        if (memo && !skip && d.nodes <= 0xFFFFFFFFull) {
             const uint32_t cnt = (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES];
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             if (k.ok) {
@@ -178,6 +184,8 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
         status = d.template try_next<C_LANES>(a, evc, s_bal, lane, limit);
         if (d.depth > dep0 && status < 0) {       // entered a new node (and the search goes on)
             entry[dep0 * C_LANES] = (uint32_t)d.nodes;
+        }
+        if (memo && d.depth > dep0 && status < 0) {
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             uint32_t cnt = 0;
             bool hit = false;
@@ -277,7 +285,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
         do {
             const bool was = skip;
             status = memo_step<MODEL, G, LT>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch, mask,
-                                                 &L.entry[0][lane], skip);
+                                                 &L.entry[0][lane], skip, p.memo_after);
             if constexpr (ST) hits += (!was && skip) ? 1u : 0u;
             ++iter;
             if (p.giant_cap && iter >= p.giant_cap && status < 0) {

@@ -95,7 +95,7 @@ def test_random_any_shape(ctx, model):
     _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
 
 
-DEFAULTS = {"stage0_budget": 32, "stage0_grid": 65536, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
+DEFAULTS = {"stage0_budget": 32, "memo_after": 32, "stage0_grid": 65536, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
             "wave_grid": 0, "split_budget": 1024, "memo_lane_entries": 128, "memo_grid": 0, "split_xmemo": 1,
             "memo_lds": 1, "memo_lds_entries": 64, "dag_states": 128, "memo_lds_cap": 0}
 
@@ -203,6 +203,19 @@ def test_sharded_heavy_list(ctx, knobs, n, heavy, grid):
     knobs(stage0_budget=4, heavy_mode=heavy, stage0_grid=grid)
     hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 11, n)
     _compare(ctx, gen.CONFIGS["bank_4x16_bugs"]["model_id"], hdr, ev, max_nodes=10**7)
+
+
+@pytest.mark.parametrize("name,n,budget,max_nodes", [("bank_4x16_bugs", 50000, 8, 0), ("bank_4x16", 50000, 4, 0),
+                                                     ("bank_4x16_bugs", 20000, 8, 300), ("bank_6x24", 20000, 8, 0)])
+@pytest.mark.parametrize("memo_after", [1, 24, 100, 1 << 40])
+def test_lane_mode_memo_after(ctx, knobs, name, n, budget, max_nodes, memo_after):
+    """Lane mode with the memo joining a search only after `memo_after`
+    nodes (a short search runs as the plain DFS; 2^40: never): node counts,
+    verdicts and witnesses stay the reference's (nodes entered before the
+    memo joins are still recorded when they fail)."""
+    knobs(heavy_mode=1, memo_lds=0, memo_after=memo_after, stage0_budget=budget, stage0w_budget=budget)
+    hdr, ev, _ = gen.generate_config(name, 7, n)
+    _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
 
 
 LANE_CASES = [("bank_4x16_bugs", 50000, 64, 0), ("bank_4x16_bugs", 20000, 8, 300), ("bank_4x16", 50000, 16, 0),
