@@ -331,7 +331,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra BASELINE configs")
     ap.add_argument("--stage0-budget", type=int, default=None,
-                    help="stage-0 node budget (default 20 with calls in flight, the library's otherwise)")
+                    help="stage-0 node budget (default 18 with calls in flight, the library's otherwise)")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
                     help="qsmd_set_param on every context (tuning; repeatable)")
     ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")
@@ -425,10 +425,10 @@ def main():
 
     # with calls in flight the heavy stage of one call overlaps the next call's
     # stage 0, so a lower stage-0 budget pays: since the heavy list is sharded
-    # (round 4) 19-22 measure best on config 2 at this command (7.63-8.07e9;
-    # 7.59 at 26, 7.41-7.45 at 17, 6.7 at 16, 2.2 at 14; tools/gpu/r04_budget2.sh,
-    # tools/gpu/r04_shard.sh)
-    budget0 = args.stage0_budget if args.stage0_budget is not None else (20 if S > 1 else -1)
+    # and lane mode's memo joins after 32 nodes (round 4), 17-20 measure
+    # within the spread on config 2 at this command (7.90-8.30e9 at 18; 7.6-7.7
+    # at 16; 7.59 at 26 before; tools/gpu/r04_budget3.sh)
+    budget0 = args.stage0_budget if args.stage0_budget is not None else (18 if S > 1 else -1)
     knobs = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in args.param]
     # with calls in flight the heavy stage runs in lane mode (64 searches per
     # wavefront: a few dozen wavefronts beside the next call's stage 0) with

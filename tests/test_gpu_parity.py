@@ -590,7 +590,7 @@ def test_device_resident_full_size(ctx, name, n):
 
 @pytest.mark.parametrize("name,n", [("bank_4x16", 1_000_000), ("bank_4x16_bugs", 1_250_000)])
 def test_bench_knobs_in_flight_full_size(name, n):
-    """bench.py's own knob set at full size: stage-0 budget 20, the heavy
+    """bench.py's own knob set at full size: stage-0 budget 18, the heavy
     stage in lane mode with HBM memo tables (heavy_mode 1, memo_lds 0), three
     contexts on three streams with calls in flight (each context's second
     call sizes its tail grids and lane tables from its first), on config 2
@@ -609,7 +609,7 @@ def test_bench_knobs_in_flight_full_size(name, n):
              torch.zeros(8, dtype=torch.int64, device=dev)) for _ in range(3)]
     try:
         for c in ctxs:
-            c.set_stage0_budget(20)
+            c.set_stage0_budget(18)
             c.set_param("heavy_mode", 1)
             c.set_param("memo_lds", 0)
         results = []
