@@ -529,7 +529,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const size_t off_tn = off_ts + align_up(n_tk);
     const size_t off_tw = off_tn + align_up(n_tk * 8);
     const size_t off_nd = off_tw + (want_w ? align_up(n_tk * kTaskWitness) : 0);   // nodes if the caller has none
-    const size_t off_tot = off_nd + (early && !nodes ? align_up(n_hist * 8) : 0);
+    const size_t off_rs = off_nd + (early && !nodes ? align_up(n_hist * 8) : 0);   // stage 0's saved states
+    const size_t off_tot = off_rs + (lane ? align_up(kShards * cap32 * kResumeWords * 4) : 0);
     const size_t need = off_tot + align_up(sizeof(qsmd_totals));
     bool re = false;
     rc = grow(c, &c->ws, &c->ws_bytes, need, &re);
@@ -543,6 +544,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     uint32_t* l0 = reinterpret_cast<uint32_t*>(c->ws + off_l0);
     uint32_t* h32 = reinterpret_cast<uint32_t*>(c->ws + off_h32);
     uint32_t* shards = reinterpret_cast<uint32_t*>(c->ws + kOffShards);
+    uint32_t* states = lane ? reinterpret_cast<uint32_t*>(c->ws + off_rs) : nullptr;
     uint32_t* h64 = reinterpret_cast<uint32_t*>(c->ws + off_h64);
     uint32_t* lw = reinterpret_cast<uint32_t*>(c->ws + off_lw);
     uint32_t* lg = reinterpret_cast<uint32_t*>(c->ws + off_lg);
@@ -577,6 +579,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.heavy_list = h32;
     a0.heavy_count = shards;
     a0.heavy_shard_cap = (uint32_t)cap32;
+    a0.heavy_state = states;                 // (lane mode goes on from them)
     a0.stage0_budget = c->stage0_budget ? c->stage0_budget : ~0ull;
     a0.stamps = c->s0_stamps;
     const uint64_t n_groups = std::max<uint64_t>((n_hist + 63) / 64, 1);
@@ -620,6 +623,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].table = reinterpret_cast<uint32_t*>(c->mt + (w ? slots * 32 : 0));
             mp[w].entries = (uint32_t)c->mt_entries;
             mp[w].memo_after = (uint32_t)std::min<uint64_t>(c->memo_after, 0xFFFFFFFFull);
+            mp[w].resume = w ? nullptr : states;
             mp[w].lds_entries = lds_entries;
             mp[w].epoch = c->mt_epoch;
             mp[w].giant_cap = cap;

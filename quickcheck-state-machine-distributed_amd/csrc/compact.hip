@@ -77,6 +77,7 @@ __device__ __forceinline__ int run_search(DFS& dfs, const SearchArgs& a, const u
         } else if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
             atomicOr(a.timed_out, 1u);
             status = QSMD_STATUS_BUDGET;
+            dfs.last_j = 32u;          // (no untried candidate: LaneDFS::save)
         }
         if (status >= 0) break;
     }
@@ -221,8 +222,12 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
         const bool heavy = tiered && status == QSMD_STATUS_BUDGET && dfs.nodes >= limit;
         if (a.heavy_shard_cap) {    // (stage 0: the group's shard, internal.h)
             const uint32_t k = (uint32_t)((base / C_LANES) % kShards);
-            wave_append(heavy, h, a.heavy_list + (uint64_t)k * a.heavy_shard_cap, a.heavy_count + k * kShardStride,
-                        lane);
+            const uint32_t at = wave_append(heavy, h, a.heavy_list + (uint64_t)k * a.heavy_shard_cap,
+                                            a.heavy_count + k * kShardStride, lane);
+            if constexpr (G::EV == 32) {
+                if (heavy && a.heavy_state)
+                    dfs.save(a.heavy_state + ((uint64_t)k * a.heavy_shard_cap + at) * kResumeWords, s_bal, lane);
+            }
         } else {
             wave_append(heavy, h, a.heavy_list, a.heavy_count, lane);
         }

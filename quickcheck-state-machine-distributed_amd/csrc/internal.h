@@ -73,6 +73,8 @@ enum Cnt : uint32_t {
 // entries are list[k * cap .. k * cap + count_k), cap = that bound x 64.
 // Consumers see one list through list_total / list_at (index order: shard
 // 0's entries, then shard 1's, ...).
+// words of a saved stage-0 search state (LaneDFS::save / restore, lane.h)
+constexpr uint32_t kResumeWords = 20;
 constexpr uint32_t kShards = 16;
 constexpr uint32_t kShardStride = 64;
 
@@ -87,14 +89,18 @@ __device__ __forceinline__ uint32_t list_total(const uint32_t* count, uint32_t c
     for (uint32_t k = 0; k < kShards; ++k) t += count[k * kShardStride];
     return t;
 }
-__device__ __forceinline__ uint32_t list_at(const uint32_t* list, const uint32_t* count, uint32_t cap, uint64_t idx) {
-    if (!cap) return list[idx];
+// the position in `list` of entry idx
+__device__ __forceinline__ uint64_t list_pos(const uint32_t* count, uint32_t cap, uint64_t idx) {
+    if (!cap) return idx;
     for (uint32_t k = 0; k < kShards; ++k) {
         const uint32_t c = count[k * kShardStride];
-        if (idx < c) return list[(uint64_t)k * cap + idx];
+        if (idx < c) return (uint64_t)k * cap + idx;
         idx -= c;
     }
     return 0u;   // (idx >= list_total: not reached)
+}
+__device__ __forceinline__ uint32_t list_at(const uint32_t* list, const uint32_t* count, uint32_t cap, uint64_t idx) {
+    return list[list_pos(count, cap, idx)];
 }
 
 // Workspace header: counters, buckets (normal and early-exit recount), the
@@ -125,6 +131,8 @@ struct SearchArgs {
     uint32_t* heavy_list;
     uint32_t* heavy_count;
     uint32_t heavy_shard_cap;     // > 0: heavy_list / heavy_count sharded (kShards)
+    uint32_t* heavy_state;        // stage 0: a heavy history's search state at the budget, at its list
+                                  // position (kResumeWords words; null = the heavy stage starts at the root)
     uint64_t stage0_budget;
     uint32_t flags;
     uint32_t model_id;
@@ -292,6 +300,7 @@ struct MemoArgs {
     uint32_t* table;              // grid * 64 * entries * (8 | 16) u32
     uint32_t entries;
     uint32_t memo_after;          // no memo probe / insert before a search has counted this many nodes
+    const uint32_t* resume;       // G32 list: stage 0's saved states (SearchArgs::heavy_state), or null
     uint32_t lds_entries;         // LDS tables (lds_tables): entries per lane, a power of two <= 64
     uint32_t epoch;               // this call's tag (24 bits)
     uint64_t giant_cap;           // > 0: a search past this many iterations goes to s.giant_list

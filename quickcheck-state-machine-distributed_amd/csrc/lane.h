@@ -478,7 +478,8 @@ struct LaneDFS {
     uint32_t depth, ex, RS, found;
     int32_t neg;            // < 0: some existing balance is negative (the invariant fails)
     uint32_t base;          // depth of the search root (0; the task depth in split_search)
-    uint32_t last_j;        // candidate of the most recent try (the one a BUDGET return did not count)
+    uint32_t last_j;        // candidate of the most recent try (the one a BUDGET return did not count;
+                            // 32: none -- a BUDGET from the time limit, compact.hip run_search)
     uint64_t nodes;
     StackN<G::LEVELS / 4> stk;
 
@@ -686,18 +687,56 @@ struct LaneDFS {
         for (uint32_t d = 0; d < depth; ++d) w[d] = (uint8_t)(stk.get(d, depth) & JM);
         if (depth < n_ev) w[depth] = QSMD_WITNESS_END;
     }
+
+    // The search state at a stage budget (a BUDGET return: nothing moved but
+    // the untried candidate last_j, dropped from cand), for the heavy stage
+    // to go on from instead of the root (G32 only: kResumeWords words --
+    // rem, cand, depth, found, ex, neg, RS, nodes, the stack, the balances)
+    __device__ __forceinline__ void save(uint32_t* r, int32_t (*s_bal)[C_LANES], int lane) const {
+        static_assert(sizeof(M) == 4 && G::LEVELS / 4 == 4, "G32");
+        uint4* q = reinterpret_cast<uint4*>(r);
+        q[0] = make_uint4(rem, cand | (last_j < 32u ? 1u << last_j : 0u), depth, found);
+        q[1] = make_uint4(ex, (uint32_t)neg, RS, (uint32_t)nodes);
+        q[2] = make_uint4(stk.w[0], stk.w[1], stk.w[2], stk.w[3]);
+        if constexpr (BANK) {
+            q[3] = make_uint4((uint32_t)s_bal[0][lane], (uint32_t)s_bal[1][lane], (uint32_t)s_bal[2][lane],
+                              (uint32_t)s_bal[3][lane]);
+            q[4] = make_uint4((uint32_t)s_bal[4][lane], (uint32_t)s_bal[5][lane], (uint32_t)s_bal[6][lane],
+                              (uint32_t)s_bal[7][lane]);
+        }
+    }
+    // (after init() from the staged history)
+    __device__ __forceinline__ void restore(const uint32_t* r, int32_t (*s_bal)[C_LANES], int lane) {
+        static_assert(sizeof(M) == 4 && G::LEVELS / 4 == 4, "G32");
+        const uint4* q = reinterpret_cast<const uint4*>(r);
+        const uint4 a = q[0], b = q[1], c = q[2];
+        rem = a.x; cand = a.y; depth = a.z; found = a.w;
+        ex = b.x; neg = (int32_t)b.y; RS = b.z; nodes = b.w;
+        stk.w[0] = c.x; stk.w[1] = c.y; stk.w[2] = c.z; stk.w[3] = c.w;
+        if constexpr (BANK) {
+            const uint4 d = q[3], e = q[4];
+            s_bal[0][lane] = (int32_t)d.x; s_bal[1][lane] = (int32_t)d.y;
+            s_bal[2][lane] = (int32_t)d.z; s_bal[3][lane] = (int32_t)d.w;
+            s_bal[4][lane] = (int32_t)e.x; s_bal[5][lane] = (int32_t)e.y;
+            s_bal[6][lane] = (int32_t)e.z; s_bal[7][lane] = (int32_t)e.w;
+        }
+    }
 };
 
 // Wave-aggregated append of h to list (one atomic per wavefront).
-__device__ __forceinline__ void wave_append(bool pred, uint32_t h, uint32_t* list, uint32_t* count, int lane) {
+// Returns the lane's slot (meaningful where pred).
+__device__ __forceinline__ uint32_t wave_append(bool pred, uint32_t h, uint32_t* list, uint32_t* count, int lane) {
     const uint64_t dm = __ballot(pred);
+    uint32_t at = 0;
     if (dm) {
         const int leader = __builtin_ctzll(dm);
         uint32_t slot = 0;
         if (lane == leader) slot = atomicAdd(count, (uint32_t)__builtin_popcountll(dm));
         slot = __shfl(slot, leader, 64);
-        if (pred) list[slot + lane_prefix(dm)] = h;
+        at = slot + lane_prefix(dm);
+        if (pred) list[at] = h;
     }
+    return at;
 }
 
 struct Counters {

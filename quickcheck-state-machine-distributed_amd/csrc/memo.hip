@@ -118,6 +118,8 @@ __device__ __forceinline__ void memo_insert(uint32_t* tab, const MemoKey<MODEL, 
 // the CUs (api.hip); fewer entries per lane (knob memo_lds_entries) leave
 // the CU's LDS to other work.  Word 0 holds the history index; kNoHistory = empty.
 constexpr uint32_t kNoHistory = 0xFFFFFFFFu;
+// an entry count never recorded (a level entered by stage 0 before a resume)
+constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
 
 template <uint32_t MODEL, class G>
 __device__ __forceinline__ bool memo_lookup_lds(const uint32_t* col, const MemoKey<MODEL, G>& k, uint32_t h,
@@ -166,7 +168,7 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     if (empty & !term) {
         // leaving the node at depth d.depth: its subtree was searched to the end and failed
         // (counts kept mod 2^32: exact while the running count is below 2^32)
-        if (memo && !skip && d.nodes <= 0xFFFFFFFFull) {
+        if (memo && !skip && d.nodes <= 0xFFFFFFFFull && entry[(d.depth - 1u) * C_LANES] != kNoEntry) {
             const uint32_t cnt = (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES];
             const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             if (k.ok) {
@@ -247,7 +249,8 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
     uint64_t r0 = 0, c0 = 0;
     uint32_t hits = 0;
     if constexpr (ST) r0 = __builtin_amdgcn_s_memrealtime();
-    const uint32_t h = active ? list_at(a.list, a.list_count, a.list_shard_cap, idx) : 0u;
+    const uint64_t pos = active ? list_pos(a.list_count, a.list_shard_cap, idx) : 0u;
+    const uint32_t h = active ? a.list[pos] : 0u;
     qsmd_hdr H;
     if (active) H = a.hdr[h];
     else H = qsmd_hdr{0, 0, 0, 0, 0, 0};
@@ -278,6 +281,15 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
     } else {
         dfs.init(s, a, L.bal, lane);
         search = true;
+        if constexpr (G::EV == 32) {
+            // go on from stage 0's state at its budget (the nodes it counted
+            // stay counted); the levels entered there have no entry count,
+            // so they are never recorded in the memo when they fail
+            if (p.resume) {
+                dfs.restore(p.resume + pos * kResumeWords, L.bal, lane);
+                for (uint32_t d = 0; d < dfs.depth; ++d) L.entry[d][lane] = kNoEntry;
+            }
+        }
     }
     if (search) {
         bool skip = false;

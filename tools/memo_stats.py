@@ -71,6 +71,9 @@ def main():
         "group_span_us": {"median": round(float(np.median(span)), 1), "max": round(float(span.max()), 1)},
         "max_iterations": {"median": int(np.median(q[:, 3])), "max": int(q[:, 3].max())},
         "iterations_total": int(q[:, 4].sum()),
+        "lane_utilisation": round(float(q[:, 4].sum()) / float((q[:, 3] * 64).sum()), 3),
+        "iterations_per_history": {"mean": round(float(q[:, 4].sum()) / float(q[:, 6].sum()), 1)},
+        "max_over_mean_per_group": {"median": round(float(np.median(q[:, 3] / np.maximum(q[:, 4] / np.maximum(q[:, 6], 1), 1))), 2)},
         "memo_hits_total": int(q[:, 5].sum()),
         "cycles_per_iteration": {"median": round(float(np.median(cyc_per_it)), 0),
                                  "of_longest_group": round(float(cyc_per_it[worst]), 0)},
