@@ -603,7 +603,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     aw.stage0_budget = c->stage0w_budget ? c->stage0w_budget : ~0ull;
     if (!(route & kSkip0w))
         HIP_TRY(c, launch_compact64(aw, (uint32_t)((route & kSkip0) ? std::min<uint64_t>(n_groups, kStage0wGrid)
-                                                                    : tail_grid(2ull * c->n_cu, kStage0wGrid, hint[0])),
+                                                                    : (hint[0] == 0u ? 8u   // (last call: none)
+                                                                                     : tail_grid(2ull * c->n_cu, kStage0wGrid,
+                                                                                                 hint[0]))),
                                     s), "stage 0w launch");
     stage_done("stage0w", s, cnt);
     // ---- heavy stage: histories over the stage budgets
