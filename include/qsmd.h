@@ -241,6 +241,9 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *                       state DAG (default 128, items 4x that; 0 = the DFS
  *                       for every history); a history whose DAG does not fit
  *                       runs the DFS
+ *   "memo_after"        lane mode: the memo joins a search after this many
+ *                       nodes (default 32; before, the plain DFS without the
+ *                       probe per node)
  *   "giant_grid"        giant stage workgroups (0 = 2 per CU, or 64 when the
  *                       last finished call had no giant history)
  *   "wave_stats_ptr", "memo_stats_ptr", "memo_stats_groups"  diagnostics:
