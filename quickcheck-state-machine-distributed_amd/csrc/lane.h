@@ -131,6 +131,13 @@ __device__ __forceinline__ int32_t bank_sign(uint32_t code) {
     return __builtin_amdgcn_sbfe((int32_t)kBankSign, code * 2u, 2u);
 }
 
+// (x & m) | y as one v_and_or_b32 (hipcc makes two of them two ands and an or3)
+__device__ __forceinline__ uint32_t and_or(uint32_t x, uint32_t m, uint32_t y) {
+    uint32_t d;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(d) : "v"(x), "s"(m), "v"(y));
+    return d;
+}
+
 // (x << s) | y as one v_lshl_or_b32 (hipcc merges two of them into
 // shifts and an or3)
 __device__ __forceinline__ uint32_t lshl_or(uint32_t x, uint32_t s, uint32_t y) {
@@ -637,7 +644,7 @@ struct LaneDFS {
             // with m exactly when the step's sign is non-zero: insertWith),
             // then Transfer's deposit on b; stored unconditionally (the old
             // values when !ok)
-            stw = j | ((uint32_t)exm & (1u << JB)) | ((uint32_t)exbm & (2u << JB));
+            stw = and_or((uint32_t)exbm, 2u << JB, and_or((uint32_t)exm, 1u << JB, j));
             const int32_t sa = bank_sign(code);
             const int32_t na = (bal_a & exm) + (sa & (exm | 1)) * m;
             const int32_t bo = same ? na : bal_b;
