@@ -111,6 +111,10 @@ class InFlight:
         self.comm = (comm or torch.cuda.Stream(dev)) if use_dist else None
         self.do_ar = use_dist and os.environ.get("QSMD_BENCH_NOAR") != "1"
         self.done = [None, None]
+        # the per-call timing events inside the timed window (the roofline
+        # leg after it always records them): instrumentation only -- the
+        # headline runs without (api.hip: ~13 us per call for a lone caller)
+        self.timing_events = 1
         self.k = 0
         self.last = (0, 0)
 
@@ -166,6 +170,8 @@ class InFlight:
             dist.barrier(group=self.host_group)
         torch.cuda.synchronize(self.dev)
         self.ctxs[0].timing_reset()
+        for c in self.ctxs:
+            c.set_param("timing_events", self.timing_events)
         t0 = time.perf_counter()
         for _ in range(steps):
             self.step()
@@ -178,6 +184,8 @@ class InFlight:
         # inside the window; a last partial block is reduced after it (one
         # collective's latency in a 20-step run was ~10 %)
         elapsed = time.perf_counter() - t0
+        for c in self.ctxs:
+            c.set_param("timing_events", 1)
         self.drain()
         torch.cuda.synchronize(self.dev)
         if self.use_dist:
@@ -337,6 +345,9 @@ def main():
     ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP initialises)")
+    ap.add_argument("--timing-events", type=int, default=0, choices=(0, 1),
+                    help="per-call HIP timing events inside the timed window (1: device_ms.in_flight; "
+                         "instrumentation, ~13 us per synchronous call)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="calls in flight (one context + stream each); 0 = 3")
     ap.add_argument("--ar-rounds", type=int, default=16,
@@ -443,6 +454,7 @@ def main():
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
     run = InFlight(dev, model_id, d_hdr, n, d_ev, len(ev), S, max(1, args.ar_rounds), flags, use_dist, knobs,
                    budget0, streams, host_group, comm)
+    run.timing_events = args.timing_events
     elapsed = run.timed(args.steps, args.warmup)
     s0_ms, call_ms = run.ctxs[0].timing_read()
     st, nd, tot = run.results()

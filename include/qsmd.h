@@ -204,14 +204,19 @@ int qsmd_set_time_limit_ms(qsmd_ctx* ctx, uint64_t ms);
  * Default 65536.  Does not change any result. */
 int qsmd_set_stage0_grid(qsmd_ctx* ctx, uint64_t max_blocks);
 
-/* Tuning knob: node budget of the first search stage (default 32; 0 = none).
- * A history whose search needs more nodes is searched again, from the root,
- * by the heavy stage (one lane per history with an exact-count state memo),
- * so one long search does not hold 63 idle lanes.  Results are unchanged. */
+/* Tuning knob: node budget of the first search stage (0 = none).  A history
+ * whose search needs more nodes goes on in the heavy stage (one lane per
+ * history with an exact-count state memo, from the saved search state; or
+ * one wavefront per history), so one long search does not hold 63 idle
+ * lanes.  Default (until set; knob "stage0_budget_auto" 1 restores it):
+ * automatic -- 32, or 16 while the context's last finished call sent fewer
+ * than 1 in 50 histories to the heavy stage, back to 32 above 1 in 5.
+ * Results are unchanged. */
 int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
 
 /* Tuning knobs by name (none changes a result):
  *   "stage0_budget"     as qsmd_set_stage0_budget
+ *   "stage0_budget_auto" 1: the automatic stage-0 budget (the default)
  *   "stage0w_budget"    the same for 33..64-event histories (default 32)
  *   "stage0_grid"       as qsmd_set_stage0_grid
  *   "split_budget"      as qsmd_set_split_budget
@@ -244,6 +249,9 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *   "memo_after"        lane mode: the memo joins a search after this many
  *                       nodes (default 32; before, the plain DFS without the
  *                       probe per node)
+ *   "timing_events"     1: record the per-call timing events (qsmd_timing_read,
+ *                       qsmd_last_kernel_ms); 0 (default until
+ *                       qsmd_timing_reset): none
  *   "giant_grid"        giant stage workgroups (0 = 2 per CU, or 64 when the
  *                       last finished call had no giant history)
  *   "wave_stats_ptr", "memo_stats_ptr", "memo_stats_groups"  diagnostics:
@@ -376,10 +384,13 @@ int qsmd_wellformed_batch_device(qsmd_ctx* ctx, const qsmd_hdr* hdr_dev, uint64_
                                  void* stream);
 
 /* Device time (ms, HIP events on the launch stream) of the search kernels of
- * the most recent check call, measured once that stream has completed. */
+ * the most recent timed check call, measured once that stream has completed.
+ * Timing is off until qsmd_timing_reset (or knob "timing_events" 1): the
+ * events are three packets per call on the caller's stream. */
 int qsmd_last_kernel_ms(qsmd_ctx* ctx, float* ms_out);
 
-/* Per-call device timings since the last reset (at most the last 1024 calls):
+/* Per-call device timings since the last reset, which also turns timing on
+ * (at most the last 1024 calls):
  * stage0_ms[i] = the first (dominant) search kernel (0 when the host entry
  * skipped stage 0: no history of the call fitted it), call_ms[i] = every
  * kernel of call i.  Synchronises on the recorded events. */

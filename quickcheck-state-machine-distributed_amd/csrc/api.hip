@@ -59,9 +59,21 @@ struct qsmd_ctx {
     std::vector<uint8_t> ev_no0;       // per slot: stage 0 skipped (its end event not recorded)
     uint64_t n_calls = 0;              // calls recorded since the last reset
     bool timed = false;
+    // the per-call timing events above are recorded (from qsmd_timing_reset
+    // on, or knob timing_events): three event packets per call that a lone
+    // caller pays ~13 us a call for (one call at a time 4.32 vs 4.59e9 with
+    // and without, tools/gpu/r04_tev.sh), so off until asked for
+    bool timing = false;
     uint64_t time_limit_ms = 120000;   // safety net per search launch
     uint64_t stage0_max_grid = 65536;  // tuning: cap on stage-0 workgroups (grid-stride beyond)
-    uint64_t stage0_budget = 32;       // stage-0 node budget before the heavy stage
+    uint64_t stage0_budget = 32;       // stage-0 node budget before the heavy stage (when not automatic)
+    // automatic stage-0 budget (until a budget is set): 32, or 16 while the
+    // last finished call's stage 0 sent few histories to the heavy stage --
+    // one call at a time on config 2: 4.78 vs 4.59e9 (the heavy list long
+    // enough for lane mode, whose tail is no longer than wave mode's, behind
+    // a shorter stage 0); config 3's bug-laden batches keep 32 (their heavy
+    // fraction at 16 is far above the threshold)
+    bool s0_auto = true;
     uint64_t stage0w_budget = 32;      // stage-0w node budget before the heavy stage
     uint64_t split_budget = 1024;      // giant stage: whole-search iterations = 16x, heavy-stage cap = 64x
     uint64_t wave_grid = 0;            // heavy stage, wave mode: workgroups (0 = from the last call's heavy count)
@@ -296,9 +308,25 @@ void qsmd_close(qsmd_ctx* c) {
     delete c;
 }
 
+static constexpr uint64_t kAutoLo = 16, kAutoHi = 32;
+
+// the stage-0 budget of this call: the set one, or (automatic) from the last
+// finished call's probe -- at 16, back to 32 once more than 1 in 5 of its
+// histories went on to the heavy stage; at 32, down to 16 while fewer than 1
+// in 50 did (the gap between the two keeps a batch from alternating)
+static uint64_t stage0_budget_of(const qsmd_ctx* c, const uint32_t* hint) {
+    if (!c->s0_auto) return c->stage0_budget;
+    if (!c->probe_valid) return kAutoHi;
+    const uint64_t heavy = hint[1], n = hint[kProbeN], last = hint[kProbeBudget];
+    if (!n) return last == kAutoLo ? kAutoLo : kAutoHi;
+    if (last == kAutoLo) return heavy * 5 > n ? kAutoHi : kAutoLo;
+    return heavy * 50 < n ? kAutoLo : kAutoHi;
+}
+
 int qsmd_set_stage0_budget(qsmd_ctx* c, uint64_t nodes) {
     if (!c) return QSMD_ERR_ARG;
     c->stage0_budget = nodes;
+    c->s0_auto = false;
     return QSMD_OK;
 }
 
@@ -308,6 +336,10 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     const std::string n(name);
     if (n == "stage0_budget") {
         c->stage0_budget = value;
+        c->s0_auto = false;
+    } else if (n == "stage0_budget_auto") {
+        if (value > 1) return fail(c, QSMD_ERR_ARG, "stage0_budget_auto: 0 or 1");
+        c->s0_auto = value != 0;
     } else if (n == "stage0w_budget") {
         c->stage0w_budget = value;
     } else if (n == "stage0_grid") {
@@ -347,6 +379,9 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         if (value < 4 || value > 64 || (value & (value - 1)))
             return fail(c, QSMD_ERR_ARG, "memo_lds_entries: a power of two in 4..64");
         c->memo_lds_entries = (uint32_t)value;
+    } else if (n == "timing_events") {     // 0: no per-call timing events (qsmd_timing_read / last_kernel_ms)
+        if (value > 1) return fail(c, QSMD_ERR_ARG, "timing_events: 0 or 1");
+        c->timing = value != 0;
     } else if (n == "memo_after") {
         c->memo_after = value;
     } else if (n == "memo_lds_cap") {       // diagnostic: force the LDS-refused path (the HBM tables)
@@ -488,8 +523,14 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // hint: every tail kernel is grid-stride, any grid gives the same
     // results); none before a call has finished
     if (!c->probe_valid && c->any_call && hipEventQuery(c->done_ev) == hipSuccess) c->probe_valid = true;
-    uint32_t hint[6];
-    for (int i = 0; i < 6; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
+    uint32_t hint[8];
+    for (int i = 0; i < 8; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
+    const uint64_t budget0 = stage0_budget_of(c, hint);
+    // the automatic budget just went down: the last call's heavy count (at
+    // the higher budget) undercounts this one's -- size the tail for a long
+    // list (a caller that runs ahead enqueues many calls on that stale hint)
+    if (c->s0_auto && c->probe_valid && budget0 < hint[kProbeBudget])
+        hint[1] = std::max<uint32_t>(hint[1], (uint32_t)std::min<uint64_t>(n_hist / 4, 0xFFFFFFFEull));
     // heavy-stage mode: lane mode (64 searches per wavefront instruction) for
     // a long heavy list, wave mode (one search per wavefront, its DFS chain
     // ~10x shorter) for a short one -- by the last finished call's count
@@ -570,6 +611,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
 
     c->ws_dirty = true;                 // until the giant stage is enqueued
     hipEvent_t* evs = &c->ev[3 * (c->n_calls % kTimingSlots)];
+    const bool tm = c->timing;
     // ---- stage 0: every history, <= 32 events
     SearchArgs a0 = a;
     a0.list = nullptr;
@@ -580,17 +622,18 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.heavy_count = shards;
     a0.heavy_shard_cap = (uint32_t)cap32;
     a0.heavy_state = states;                 // (lane mode goes on from them)
-    a0.stage0_budget = c->stage0_budget ? c->stage0_budget : ~0ull;
+    a0.stage0_budget = budget0 ? budget0 : ~0ull;
     a0.stamps = c->s0_stamps;
     const uint64_t n_groups = std::max<uint64_t>((n_hist + 63) / 64, 1);
     stage_done("start", s, cnt);
     if (!(route & kSkip0)) {           // (the events at the kernel's start and end)
-        HIP_TRY(c, launch_compact(a0, (uint32_t)std::min<uint64_t>(n_groups, c->stage0_max_grid), s, evs[0], evs[1]),
+        HIP_TRY(c, launch_compact(a0, (uint32_t)std::min<uint64_t>(n_groups, c->stage0_max_grid), s,
+                                  tm ? evs[0] : nullptr, tm ? evs[1] : nullptr),
                 "stage 0 launch");
-    } else {                           // (no stage-0 end event: one packet less before the first kernel)
+    } else if (tm) {                   // (no stage-0 end event: one packet less before the first kernel)
         HIP_TRY(c, hipEventRecord(evs[0], s), "hipEventRecord");
     }
-    c->ev_no0[c->n_calls % kTimingSlots] = (route & kSkip0) ? 1u : 0u;
+    if (tm) c->ev_no0[c->n_calls % kTimingSlots] = (route & kSkip0) ? 1u : 0u;
     stage_done("stage0", s, cnt);
     // ---- stage 0w: the rest, <= 64 events (beyond: the giant stage)
     SearchArgs aw = a;
@@ -691,6 +734,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     p.early = early ? 1u : 0u;
     p.totals = tot;
     p.probe_host = c->probe_host;
+    p.probe_budget = (uint32_t)std::min<uint64_t>(budget0, 0xFFFFFFFFull);
     p.stall_ticks = c->giant_stall_us * 100ull;   // 100 MHz s_memrealtime
     if (flags & QSMD_FLAG_MEMO) {
         rc = memo_prepare(c, s, &p.memo, &p.memo_epoch);
@@ -741,13 +785,15 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     }
     stage_done("giants", s, cnt);
     c->ws_dirty = false;
-    HIP_TRY(c, hipEventRecord(evs[2], s), "hipEventRecord");
+    if (tm) HIP_TRY(c, hipEventRecord(evs[2], s), "hipEventRecord");
     HIP_TRY(c, hipEventRecord(c->done_ev, s), "hipEventRecord");
     c->last_stream = s;
     c->in_flight = true;
     c->any_call = true;
-    c->n_calls++;
-    c->timed = true;
+    if (tm) {                           // (untimed calls leave the timing ring as it was)
+        c->n_calls++;
+        c->timed = true;
+    }
     return QSMD_OK;
 }
 
@@ -944,7 +990,7 @@ int qsmd_wellformed_batch(qsmd_ctx* c, const qsmd_hdr* hdr, uint64_t n_hist, con
 
 int qsmd_last_kernel_ms(qsmd_ctx* c, float* ms) {
     if (!c || !ms) return QSMD_ERR_ARG;
-    if (!c->timed || c->n_calls == 0) return fail(c, QSMD_ERR_ARG, "no check call yet");
+    if (!c->timed || c->n_calls == 0) return fail(c, QSMD_ERR_ARG, "no timed check call yet (qsmd_timing_reset first)");
     hipEvent_t* evs = &c->ev[3 * ((c->n_calls - 1) % kTimingSlots)];
     HIP_TRY(c, hipEventSynchronize(evs[2]), "hipEventSynchronize");
     HIP_TRY(c, hipEventElapsedTime(ms, evs[0], evs[2]), "hipEventElapsedTime");
@@ -955,6 +1001,7 @@ int qsmd_timing_reset(qsmd_ctx* c) {
     if (!c) return QSMD_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
     c->n_calls = 0;
+    c->timing = true;
     return QSMD_OK;
 }
 

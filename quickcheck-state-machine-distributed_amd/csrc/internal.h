@@ -166,6 +166,8 @@ struct SearchArgs {
 // qsmd_ctx::probe_host slots: [C_DEFER, C_HEAVY32, C_HEAVY64, C_GIANT,
 // C_TIMED] of the last finished call, then its wide-list count
 constexpr int kProbeWide = 5;
+constexpr int kProbeBudget = 6;   // the call's stage-0 budget and batch size (api.hip: the automatic budget)
+constexpr int kProbeN = 7;
 
 // internal status: the search was handed to a later stage (not a result)
 constexpr int QSMD_STATUS_HANDED_OFF = 0x40;
@@ -217,6 +219,7 @@ struct SplitArgs {
     uint32_t early;               // QSMD_FLAG_EARLY_EXIT_BATCH: the fixup phase runs
     qsmd_totals* totals;          // the call's totals (device), written by the last block
     uint32_t* probe_host;         // pinned host copy of counters [0..3] (null = none)
+    uint32_t probe_budget;        // -> probe_host[kProbeBudget]: the call's stage-0 budget (saturated)
     uint32_t* debug;              // diagnostic: pinned host [grid][4] phase / progress (null = none)
     uint64_t stall_ticks;         // diagnostic (giant_stall_us): the first frontier chunk starts this late
 };

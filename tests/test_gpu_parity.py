@@ -51,6 +51,48 @@ def test_kats_on_device(ctx):
             assert replay_witness(m, hist, res.witness_of(0)), name
 
 
+def test_timing_events():
+    """Per-call timing events: off until qsmd_timing_reset (a lone caller
+    does not pay three event packets a call), then stage 0 and the whole
+    call per check call; knob timing_events 0 stops them again."""
+    c = device.Context(0)
+    try:
+        hdr, ev, _ = gen.generate_config("bank_4x16", 1, 5000)
+        c.check_arrays(models.MODEL_BANK, hdr, ev)
+        with pytest.raises(device.DeviceError):
+            c.last_kernel_ms()
+        assert len(c.timing_read()[0]) == 0
+        c.timing_reset()
+        for _ in range(2):
+            c.check_arrays(models.MODEL_BANK, hdr, ev)
+        s0, call = c.timing_read()
+        assert len(s0) == 2 and (s0 > 0).all() and (call >= s0).all()
+        assert c.last_kernel_ms() > 0
+        c.set_param("timing_events", 0)
+        st, nd, _, _ = c.check_arrays(models.MODEL_BANK, hdr, ev)
+        assert len(c.timing_read()[0]) == 2
+        st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr, ev, None, 0, 8)
+        assert (st == st_o).all() and (nd == nd_o).all()
+    finally:
+        c.close()
+
+
+def test_automatic_stage0_budget():
+    """The automatic stage-0 budget (the default until a budget is set): 32,
+    16 after a call whose heavy list was short, back to 32 after one whose
+    list was long.  Alternating config-2 batches (few heavy histories) and
+    bug-laden config-3 batches (many) moves it both ways; each call's first
+    heavy stage is then sized for the other budget's list (wave mode with a
+    long list, lane mode with a short one).  Results stay the oracle's."""
+    c = device.Context(0)
+    try:
+        batches = [(name, gen.generate_config(name, 9, 30000)) for name in ("bank_4x16", "bank_4x16_bugs")]
+        for name, (hdr, ev, _) in batches * 3 + batches[:1] * 2:
+            _compare(c, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+    finally:
+        c.close()
+
+
 def test_wire_bytes_through_the_c_abi(ctx):
     """SchedulerHistory payload bytes (the reference's wire format, built by
     hand in tests/test_wire.py) -> qsmd.wire -> qsmd_check_batch: the KATs'
