@@ -266,7 +266,7 @@ LANE_CASES = [("bank_4x16_bugs", 50000, 64, 0), ("bank_4x16_bugs", 20000, 8, 300
 
 @pytest.mark.parametrize("name,n,budget,max_nodes", LANE_CASES)
 @pytest.mark.parametrize("entries", [128, 2])
-@pytest.mark.parametrize("lds,lds_entries", [(0, 64), (2, 64), (2, 16)])
+@pytest.mark.parametrize("lds,lds_entries", [(0, 64), (2, 64), (2, 16), (2, 4)])
 def test_lane_mode(ctx, knobs, name, n, budget, max_nodes, entries, lds, lds_entries):
     """Lane mode of the heavy stage (exact-count state memo in a private
     table per lane, in HBM or, lds=2, in LDS with 64 or 16 entries per
