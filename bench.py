@@ -28,11 +28,17 @@ import time
 
 # HIP reads GPU_MAX_HW_QUEUES when it initialises (the first torch CUDA call):
 # --hw-queues Q sets it for this process before torch is imported
-# (8 unless asked otherwise, over the environment's value -- the GPU boxes
-# export HIP's default of 4): each slot stream keeps a hardware queue of its
-# own (a lone rank's 4 slots and torch's stream would share 4; with RCCL the
-# 3 slot streams, the all-reduce's own stream and RCCL's internal one)
-os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1] if "--hw-queues" in sys.argv else "8"
+if "--hw-queues" in sys.argv:
+    os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1]
+elif (int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("QSMD_BENCH_DIST") == "1") \
+        and "GPU_MAX_HW_QUEUES" not in os.environ:
+    # with RCCL: the 3 slot streams, the all-reduce's own stream and RCCL's
+    # internal one each keep a hardware queue (4 by default: they would share).
+    # (The GPU boxes export HIP's default of 4, which this leaves as it is.  A
+    # lone rank with 4 calls in flight on 8 queues measured +2-4 % on config
+    # 2, but 8 queues cost config 1 17 % and config 5 23 % at 3 in flight in
+    # the same process: tools/gpu/r04_inflight2.sh .. r04_d200.sh.)
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "quickcheck-state-machine-distributed_amd")
@@ -347,7 +353,7 @@ def main():
                     help="per-call HIP timing events inside the timed window (1: device_ms.in_flight; "
                          "instrumentation, ~13 us per synchronous call)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="calls in flight (one context + stream each); 0 = 4 on a lone rank, 3 under RCCL")
+                    help="calls in flight (one context + stream each); 0 = 3")
     ap.add_argument("--ar-rounds", type=int, default=16,
                     help="rounds of in-flight steps whose counters one RCCL all-reduce carries (N > 1)")
     ap.add_argument("--device-gen", action="store_true",
@@ -376,12 +382,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or os.environ.get("QSMD_BENCH_DIST") == "1"
-    # calls in flight: 4 on a lone rank, 3 under RCCL.  The final round-4
-    # build, the driver's command, alternating on one box: a lone rank 4 on 8
-    # queues 8.35-8.79e9 vs 3 on 4 7.62-8.11e9 (5 in flight 7.58-8.24);
-    # one rank over the RCCL path 3: 7.44-7.97e9 vs 4: 6.77-7.62e9 at 8, 12
-    # or 16 queues (tools/gpu/r04_inflight3.sh, r04_inflight4.sh)
-    S = args.inflight if args.inflight > 0 else (3 if use_dist else 4)
+    S = args.inflight if args.inflight > 0 else 3
     # the slot streams, created and used before RCCL creates its own, so that
     # each gets a hardware queue of its own (GPU_MAX_HW_QUEUES)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
