@@ -49,6 +49,12 @@ struct qsmd_ctx {
     // the calls of this context are ordered: each waits for the previous one
     // (whatever its stream), and buffers are freed only once it is done
     hipEvent_t done_ev = nullptr;
+    // the completion event is recorded only once the context has seen a
+    // second stream: a call's last packet costs a lone caller ~2-3 us (one
+    // call at a time 4.79-4.84 vs 4.71-4.76e9 without / with it,
+    // tools/gpu/r04_nodone.sh); on one stream the stream orders the calls
+    bool multi = false;                // calls on more than one stream: record done_ev every call
+    bool done_last = false;            // the last call recorded done_ev
     hipStream_t last_stream = nullptr;
     bool in_flight = false;
     bool any_call = false;             // a check call was enqueued
@@ -163,11 +169,27 @@ static bool sync_stages() {
 size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 // Wait until the context's previous call is done (its buffers may be in use).
+// (Without its completion event -- one stream so far -- the whole device: the
+// caller's stream may be gone by now.)
 void quiesce(qsmd_ctx* c) {
     if (c->in_flight) {
-        (void)hipEventSynchronize(c->done_ev);
+        if (c->done_last) (void)hipEventSynchronize(c->done_ev);
+        else (void)hipDeviceSynchronize();
         c->in_flight = false;
     }
+}
+
+// A call on stream s: the previous call of this context (on another
+// stream) comes first -- its completion event, or, the first time a second
+// stream shows up (no event recorded yet), the device; every call records
+// the event from then on.
+static hipError_t order_after_previous(qsmd_ctx* c, hipStream_t s) {
+    if (!c->in_flight || c->last_stream == s) return hipSuccess;
+    c->multi = true;
+    if (c->done_last) return hipStreamWaitEvent(s, c->done_ev, 0);
+    const hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) c->in_flight = false;
+    return e;
 }
 
 // Grow a device buffer to at least `need` bytes (1.5x steps); the previous
@@ -518,11 +540,13 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
 
     // the previous call of this context may run on another stream
-    if (c->in_flight && c->last_stream != s) HIP_TRY(c, hipStreamWaitEvent(s, c->done_ev, 0), "hipStreamWaitEvent");
+    HIP_TRY(c, order_after_previous(c, s), "order after the previous call");
     // the tail launches' grids from the last finished call's list sizes (a
     // hint: every tail kernel is grid-stride, any grid gives the same
-    // results); none before a call has finished
-    if (!c->probe_valid && c->any_call && hipEventQuery(c->done_ev) == hipSuccess) c->probe_valid = true;
+    // results); none before a call has finished (the giant stage's last
+    // block sets the probe's written flag)
+    if (!c->probe_valid && c->any_call && __atomic_load_n(&c->probe_host[kProbeWritten], __ATOMIC_ACQUIRE))
+        c->probe_valid = true;
     uint32_t hint[8];
     for (int i = 0; i < 8; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
     const uint64_t budget0 = stage0_budget_of(c, hint);
@@ -786,7 +810,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     stage_done("giants", s, cnt);
     c->ws_dirty = false;
     if (tm) HIP_TRY(c, hipEventRecord(evs[2], s), "hipEventRecord");
-    HIP_TRY(c, hipEventRecord(c->done_ev, s), "hipEventRecord");
+    if (c->multi) HIP_TRY(c, hipEventRecord(c->done_ev, s), "hipEventRecord");
+    c->done_last = c->multi;
     c->last_stream = s;
     c->in_flight = true;
     c->any_call = true;
@@ -836,7 +861,7 @@ int qsmd_check_batch(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, uint64
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     hipStream_t s = c->stream;
-    if (c->in_flight && c->last_stream != s) HIP_TRY(c, hipStreamWaitEvent(s, c->done_ev, 0), "hipStreamWaitEvent");
+    HIP_TRY(c, order_after_previous(c, s), "order after the previous call");
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness_out;
     // io layout: [hdr | events | witness] copied in, [witness | status | nodes | totals] copied out
     const size_t o_hdr = 0;

@@ -168,6 +168,7 @@ struct SearchArgs {
 constexpr int kProbeWide = 5;
 constexpr int kProbeBudget = 6;   // the call's stage-0 budget and batch size (api.hip: the automatic budget)
 constexpr int kProbeN = 7;
+constexpr int kProbeWritten = 8;  // 1 once a call's giant stage wrote the probe (never reset)
 
 // internal status: the search was handed to a later stage (not a result)
 constexpr int QSMD_STATUS_HANDED_OFF = 0x40;
