@@ -37,7 +37,7 @@ elif (int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("QSMD_BENCH_D
     # (The GPU boxes export HIP's default of 4, which this leaves as it is.  A
     # lone rank with 4 calls in flight on 8 queues measured +2-4 % on config
     # 2, but 8 queues cost config 1 17 % and config 5 23 % at 3 in flight in
-    # the same process: tools/gpu/r04_inflight2.sh .. r04_d200.sh.)
+    # the same process: tools/gpu/archive/r04_inflight2.sh .. r04_d200.sh.)
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -92,8 +92,11 @@ class InFlight:
     of steps are all-reduced together, overlapping the next block."""
 
     def __init__(self, dev, model_id, d_hdr, n, d_ev, n_ev, S, R, flags, use_dist, knobs, budget0, streams=None,
-                 host_group=None, comm=None):
-        self.dev, self.model_id, self.d_hdr, self.n, self.d_ev, self.n_ev = dev, model_id, d_hdr, n, d_ev, n_ev
+                 host_group=None, comm=None, batches=None):
+        self.dev, self.model_id, self.n = dev, model_id, n
+        # the resident batches (--rotate K: step k checks batch k % K, so the
+        # library's cross-call hints always come from another batch)
+        self.batches = batches or [(d_hdr, d_ev, n_ev)]
         self.S, self.B, self.flags = S, R * S, flags
         self.ctxs = [device.Context(dev.index) for _ in range(S)]
         for c in self.ctxs:
@@ -120,7 +123,8 @@ class InFlight:
         # headline runs without (api.hip: ~13 us per call for a lone caller)
         self.timing_events = 1
         self.k = 0
-        self.last = (0, 0)
+        self.steps_run = 0
+        self.last = (0, 0, 0, 0)
 
     def _allreduce(self, par):
         for st_ in self.streams[:-1]:
@@ -135,15 +139,17 @@ class InFlight:
         self.k += 1
         i, row, par = k % self.S, k % self.B, (k // self.B) % 2
         d_st, d_nd = self.outs[i]
+        d_hdr, d_ev, n_ev = self.batches[self.steps_run % len(self.batches)]
         with torch.cuda.stream(self.streams[i]):
             if self.done[par] is not None:
                 self.streams[i].wait_event(self.done[par])
-            self.ctxs[i].check_device(self.model_id, self.d_hdr.data_ptr(), self.n, self.d_ev.data_ptr(), self.n_ev,
+            self.ctxs[i].check_device(self.model_id, d_hdr.data_ptr(), self.n, d_ev.data_ptr(), n_ev,
                                       d_st.data_ptr(), d_nd.data_ptr(), None, self.tot[par, row].data_ptr(),
                                       flags=self.flags, stream=self.streams[i].cuda_stream)
         if self.do_ar and row == self.B - 1:
             self._allreduce(par)
-        self.last = (i, row, par)
+        self.last = (i, row, par, self.steps_run % len(self.batches))
+        self.steps_run += 1
 
     def drain(self):
         if self.k % self.B:                  # a partial last block: reduce it, start the next one fresh
@@ -156,11 +162,12 @@ class InFlight:
         sizes a context's lane-mode memo tables from its last finished call's
         heavy count (api.hip), so each context's second call may grow them
         (hipMalloc + clear); priming makes that happen outside the steps."""
+        d_hdr, d_ev, n_ev = self.batches[0]
         for i in range(self.S):
             d_st, d_nd = self.outs[i]
             with torch.cuda.stream(self.streams[i]):
-                self.ctxs[i].check_device(self.model_id, self.d_hdr.data_ptr(), self.n, self.d_ev.data_ptr(),
-                                          self.n_ev, d_st.data_ptr(), d_nd.data_ptr(), None, None, flags=self.flags,
+                self.ctxs[i].check_device(self.model_id, d_hdr.data_ptr(), self.n, d_ev.data_ptr(),
+                                          n_ev, d_st.data_ptr(), d_nd.data_ptr(), None, None, flags=self.flags,
                                           stream=self.streams[i].cuda_stream)
         torch.cuda.synchronize(self.dev)
 
@@ -176,21 +183,23 @@ class InFlight:
         self.ctxs[0].timing_reset()
         for c in self.ctxs:
             c.set_param("timing_events", self.timing_events)
+        self.steps_run = 0
         t0 = time.perf_counter()
         for _ in range(steps):
             self.step()
+        # the counters' all-reduce runs once per block of S x ar_rounds steps;
+        # the last (partial) block's runs here, inside the window: the job's
+        # only collective is part of what it times (at the driver's 20 steps
+        # it is the window's one collective)
+        self.drain()
         torch.cuda.synchronize(self.dev)
         # each rank's window runs from the common opening barrier to its own
         # GPU's end; the MAX over ranks below is the whole job's time, so the
         # closing barrier stays outside the window (inside it, its ~137 us of
-        # host gloo round trips were ~5 % of a 20-step run).
-        # The counters' all-reduce runs once per block of S x ar_rounds steps
-        # inside the window; a last partial block is reduced after it (one
-        # collective's latency in a 20-step run was ~10 %)
+        # host gloo round trips were ~5 % of a 20-step run)
         elapsed = time.perf_counter() - t0
         for c in self.ctxs:
             c.set_param("timing_events", 1)
-        self.drain()
         torch.cuda.synchronize(self.dev)
         if self.use_dist:
             dist.barrier(group=self.host_group)
@@ -201,27 +210,32 @@ class InFlight:
         return elapsed
 
     def roofline_leg(self, calls):
-        """The dominant kernel alone: `calls` synchronous calls on slot 0 (each
-        waits for the previous, nothing else on the GPU), with the stage-0
-        HIP events on the launch stream -- the per-launch time the roofline
-        divides by, and the launches a kernel trace of this command shows last
-        (profiles/summarize_pmc.py --last)."""
+        """The search kernels alone: `calls` synchronous calls of batch 0 on
+        slot 0 (each waits for the previous, nothing else on the GPU), with
+        the HIP events stage 0 and the heavy stage record at their start and
+        end on the launch stream -- the per-launch times the roofline divides
+        by, and the launches a kernel trace of this command shows last
+        (profiles/summarize_pmc.py --last).  Also returns the stage-0 budget
+        those calls ran with (the library's automatic one included)."""
         torch.cuda.synchronize(self.dev)
         self.ctxs[0].timing_reset()
         d_st, d_nd = self.outs[0]
+        d_hdr, d_ev, n_ev = self.batches[0]
         for _ in range(calls):
-            self.ctxs[0].check_device(self.model_id, self.d_hdr.data_ptr(), self.n, self.d_ev.data_ptr(), self.n_ev,
+            self.ctxs[0].check_device(self.model_id, d_hdr.data_ptr(), self.n, d_ev.data_ptr(), n_ev,
                                       d_st.data_ptr(), d_nd.data_ptr(), None, None, flags=self.flags,
                                       stream=self.streams[0].cuda_stream)
             torch.cuda.synchronize(self.dev)
-        s0, call = self.ctxs[0].timing_read()
-        return np.asarray(s0, dtype=np.float64), np.asarray(call, dtype=np.float64)
+        s0, hv, call = self.ctxs[0].timing_read_stages()
+        f64 = lambda x: np.asarray(x, dtype=np.float64)   # noqa: E731
+        return f64(s0), f64(hv), f64(call), self.ctxs[0].get_param("stage0_budget_last")
 
     def results(self):
-        i, row, par = self.last
+        """Outputs of the last step: (status, nodes, the step's totals, its batch index)."""
+        i, row, par, bi = self.last
         st = self.outs[i][0].cpu().numpy()
         nd = self.outs[i][1].cpu().numpy()
-        return st, nd, self.tot[par, row].cpu().numpy()
+        return st, nd, self.tot[par, row].cpu().numpy(), bi
 
     def close(self):
         for c in self.ctxs:
@@ -284,6 +298,66 @@ def reference_shaped(seconds):
                       f"oracle/linearise_lists.py (literal list transliteration, CPython)"}
 
 
+def early_exit_leg(dev, rank, world, config, n_per_gpu, steps, warmup, chunk, use_dist, host_group, check_oracle):
+    """BASELINE config 3's early-termination path: QSMD_FLAG_EARLY_EXIT_BATCH
+    over a batch sharded across the ranks (qsmd.dist.check_shard_early_exit_device:
+    device-resident shards, one MIN all-reduce of the first failure per
+    chunk, RCCL under torchrun).  One step = one early-exit pass over the
+    whole batch (n_per_gpu x world histories of the seeded stream); the
+    time is the MAX over ranks.  Reports the batch's histories per second
+    (every history decided: searched, or SKIPPED after the first failure as
+    QuickCheck stops at its first failing test, test/TicketDispenser.hs:284-322)
+    and the histories actually searched."""
+    from qsmd import dist as qdist
+    n_total = n_per_gpu * world
+    first, count = qdist.shard(n_total, rank, world)
+    hdr, ev, _ = gen.generate(gen.params(**gen.CONFIGS[config]), first, count, threads=min(16, host_cores()))
+    d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
+    d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
+    mid = gen.CONFIGS[config]["model_id"]
+    ctx = device.Context(dev.index)
+    run = lambda: qdist.check_shard_early_exit_device(ctx, mid, d_hdr, d_ev, len(ev), n_total, rank, world,  # noqa
+                                                      chunk=chunk, group=group)
+    for _ in range(warmup):
+        run()
+    torch.cuda.synchronize(dev)
+    if use_dist:
+        dist.barrier(group=host_group)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st, nd, info = run()
+    # the batch's totals: one SUM all-reduce (RCCL under nccl), inside the window
+    tot, _ = qdist.allreduce_totals(info["totals"], 0, None)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    searched = info["searched"]
+    if use_dist:
+        e = torch.tensor([el, float(searched)], dtype=torch.float64)
+        dist.all_reduce(e[:1], op=dist.ReduceOp.MAX, group=host_group)
+        s = e[1:].clone()
+        dist.all_reduce(s, op=dist.ReduceOp.SUM, group=host_group)
+        el, searched = float(e[0].item()), int(s.item())
+    out = {"workload": config, "histories": n_total, "histories_per_gpu": n_per_gpu, "chunk": chunk, "steps": steps,
+           "ms_per_step": el / steps * 1e3, "histories_per_sec": n_total * steps / el,
+           "searched": searched, "searched_per_sec": searched * steps / el,
+           "first_fail": info["first_fail"], "rounds": info["rounds"],
+           "totals": dict(zip(("checked", "linearisable", "nonlinearisable", "model_errors", "encode_errors",
+                               "budget", "skipped", "nodes"), (int(x) for x in tot)))}
+    if check_oracle and world == 1:
+        # the oracle on every history up to the first failure; everything after it SKIPPED
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_c
+        ff = info["first_fail"]
+        m = min(count, ff + 1)
+        st_o, nd_o, _ = oracle_c.check_batch(mid, hdr[:m], ev, threads=host_cores())
+        st_h, nd_h = st.cpu().numpy(), nd.cpu().numpy()
+        out["mismatches_vs_oracle"] = int(((st_h[:m] != st_o) | (nd_h[:m] != nd_o.astype(np.int64))).sum() +
+                                          (st_h[m:] != 5).sum())
+        out["checked_vs_oracle"] = m
+    ctx.close()
+    return out
+
+
 def extra_configs(dev, S, knobs):
     """Bounded runs of BASELINE configs 1, 3, 5 (same in-flight step as the
     headline, the library's stage-0 budget) and 4 (one adversarial 8 x 64 TicketDispenser history, memo
@@ -297,7 +371,7 @@ def extra_configs(dev, S, knobs):
         mid = gen.CONFIGS[name]["model_id"]
         run = InFlight(dev, mid, d_hdr, n, d_ev, len(ev), S, 1, device.QSMD_FLAG_EXHAUSTIVE, False, knobs, -1)
         el = run.timed(steps, 3)
-        st, nd, tot = run.results()
+        st, nd, tot, _ = run.results()
         s0, call = run.ctxs[0].timing_read()
         run.close()
         m = min(n, 50_000)
@@ -358,11 +432,21 @@ def main():
                     help="rounds of in-flight steps whose counters one RCCL all-reduce carries (N > 1)")
     ap.add_argument("--device-gen", action="store_true",
                     help="generate the batch on the GPU (qsmd_gen_batch_device; same histories as the host generator)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r04", "stage0_pmc.json"),
-                    help="PMC summary of the stage-0 kernel (profiles/summarize_pmc.py) for the roofline fields")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05", "stage0_pmc.json"),
+                    help="PMC summary of the search kernels (profiles/summarize_pmc.py) for the roofline fields")
+    ap.add_argument("--early-exit", action="store_true",
+                    help="time BASELINE config 3's early-termination path instead (bank_4x16_bugs by default, "
+                         "1.25M histories per GPU: 10M over 8 GPUs), sharded, QSMD_FLAG_EARLY_EXIT_BATCH")
+    ap.add_argument("--chunk", type=int, default=262144, help="--early-exit: histories per rank per round")
+    ap.add_argument("--rotate", type=int, default=1,
+                    help="distinct resident batches of n-hist histories; step s checks batch s %% K (the library's "
+                         "cross-call hints then come from other batches)")
     ap.add_argument("--roof-calls", type=int, default=30,
                     help="synchronous calls after the timed region that time the dominant kernel alone")
     args = ap.parse_args()
+    args.rotate = max(1, args.rotate)
+    if args.rotate > 1 and args.rotate % (args.inflight or 3) == 0:
+        ap.error("--rotate K must not be a multiple of the calls in flight (each context would see one batch)")
 
     # stdout carries exactly one JSON line (rank 0): RCCL prints a version
     # banner to file descriptor 1 when it creates its communicator, so fd 1
@@ -418,6 +502,25 @@ def main():
     # window (the counters' all-reduce stays on RCCL)
     host_group = dist.new_group(backend="gloo") if use_dist else None
 
+    if args.early_exit:
+        config = args.config if args.config != "bank_4x16" else "bank_4x16_bugs"
+        n_ee = args.n_hist if args.n_hist != 1_000_000 else 1_250_000
+        ee = early_exit_leg(dev, rank, world, config, n_ee, args.steps, args.warmup, args.chunk, use_dist, host_group,
+                            rank == 0 and not args.no_cpu_baseline)
+        if rank == 0:
+            out = {"metric": "histories decided/sec, early-termination path (QSMD_FLAG_EARLY_EXIT_BATCH, sharded)",
+                   "value": ee["histories_per_sec"], "unit": "histories/s", "n_gpus": world, "steps": args.steps,
+                   "warmup": args.warmup, "ms_per_step": ee["ms_per_step"], "higher_is_better": True,
+                   "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+                   "data": "synthetic (seeded scheduler-policy generator with injected race bugs)",
+                   "config": {"workload": config, "histories_per_gpu": n_ee, "parallelism": f"shard{world}",
+                              "chunk": args.chunk, "mode": "exhaustive + early exit"},
+                   "early_exit": ee}
+            print(json.dumps(out), file=json_out, flush=True)
+        if use_dist:
+            dist.destroy_process_group()
+        return
+
     cfg = dict(gen.CONFIGS[args.config])
     model_id = cfg["model_id"]
     n = args.n_hist
@@ -434,15 +537,23 @@ def main():
         hdr = d_hdr.cpu().numpy().view(codec.HDR_DTYPE)
         ev = d_ev.cpu().numpy().view(codec.EV_DTYPE)
     else:
-        hdr, ev, d_hdr, d_ev = device_batch(args.config, rank * n, n, dev)
-    log(f"[rank {rank}] generated {n} histories ({'device' if args.device_gen else 'host'}) "
+        hdr, ev, d_hdr, d_ev = device_batch(args.config, rank * args.rotate * n, n, dev)
+    # --rotate K: K distinct resident batches (histories [(rank K + k) n, ..)
+    # of the seeded stream); step s checks batch s % K
+    host_batches = [(hdr, ev)]
+    dev_batches = [(d_hdr, d_ev, len(ev))]
+    for k in range(1, args.rotate):
+        h_k, e_k, dh_k, de_k = device_batch(args.config, (rank * args.rotate + k) * n, n, dev)
+        host_batches.append((h_k, e_k))
+        dev_batches.append((dh_k, de_k, len(e_k)))
+    log(f"[rank {rank}] generated {args.rotate} x {n} histories ({'device' if args.device_gen else 'host'}) "
         f"in {time.perf_counter() - t:.2f}s")
 
     # with calls in flight the heavy stage of one call overlaps the next call's
     # stage 0, so a lower stage-0 budget pays: since the heavy list is sharded
     # and lane mode's memo joins after 32 nodes (round 4), 17-20 measure
     # within the spread on config 2 at this command (7.90-8.30e9 at 18; 7.6-7.7
-    # at 16; 7.59 at 26 before; tools/gpu/r04_budget3.sh)
+    # at 16; 7.59 at 26 before; tools/gpu/archive/r04_knobs2.sh)
     budget0 = args.stage0_budget if args.stage0_budget is not None else (18 if S > 1 else -1)
     knobs = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in args.param]
     # with calls in flight the heavy stage runs in lane mode (64 searches per
@@ -457,12 +568,14 @@ def main():
                 knobs.append((k, v))
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
     run = InFlight(dev, model_id, d_hdr, n, d_ev, len(ev), S, max(1, args.ar_rounds), flags, use_dist, knobs,
-                   budget0, streams, host_group, comm)
+                   budget0, streams, host_group, comm, batches=dev_batches)
     run.timing_events = args.timing_events
     elapsed = run.timed(args.steps, args.warmup)
     s0_ms, call_ms = run.ctxs[0].timing_read()
-    st, nd, tot = run.results()
-    roof_s0, roof_call = run.roofline_leg(max(1, args.roof_calls))
+    st, nd, tot, last_batch = run.results()
+    roof_s0, roof_hv, roof_call, budget_used = run.roofline_leg(max(1, args.roof_calls))
+    nd0 = run.outs[0][1].cpu().numpy()             # batch 0's node counts (the roofline leg's calls)
+    fold = run.ctxs[0].get_param("fold")
     run.close()
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -471,45 +584,70 @@ def main():
     nodes_total = int(tot[7])
     assert int(tot[0]) + int(tot[4]) + int(tot[5]) == total_hist, tot
 
-    # roofline of the dominant kernel (stage 0), rank-local: SURVEY §8d
-    # algorithmic bytes of one launch over its mean duration ALONE on the GPU
-    # (the roofline leg: synchronous calls after the timed region, HIP events
-    # on the launch stream; a kernel trace of this command shows the same
-    # launches last).  Beside it: the same bytes per step of the timed
-    # region, and what the PMC counters of a profiled run of the same
-    # configuration give for the same launches (HBM bytes moved, VALU issue).
-    t_s0 = float(np.mean(roof_s0)) * 1e-3
-    a_bytes = alg_bytes(hdr, np.minimum(nd, budget0) if budget0 > 0 else nd)
-    achieved = a_bytes / t_s0 / 1e9
-    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": a_bytes,
-            "hbm_io_bytes_per_launch": hbm_bytes(hdr), "kernel": "compact_search<Bank, G32> (stage 0)",
-            "kernel_ms": {"mean": float(np.mean(roof_s0)), "median": float(np.median(roof_s0)),
-                          "min": float(np.min(roof_s0)), "launches": int(len(roof_s0)),
-                          "call_mean": float(np.mean(roof_call)), "call_median": float(np.median(roof_call)),
-                          "how": "synchronous calls after the timed region, HIP events around stage 0"},
-            "per_step": {"achieved": a_bytes / (ms_per_step * 1e-3) / 1e9,
-                         "frac": a_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "how": "algorithmic bytes of one launch / ms_per_step (calls in flight)"}}
+    # roofline, rank-local, of the two kernels that bound a call -- stage 0
+    # and the lane-mode heavy stage -- each SURVEY §8d's algorithmic bytes of
+    # one launch over its mean duration ALONE on the GPU (the roofline leg:
+    # synchronous calls of batch 0 after the timed region, HIP events the
+    # launches record at their start and end; a kernel trace of this command
+    # shows the same launches last).  The top-level fields are the longer
+    # kernel's.  Per history: 16 B header + 16 B per operation + 16 B result
+    # + 16 B per explored node; stage 0 explores min(nodes, budget), the
+    # heavy stage re-reads its histories and explores the nodes past the
+    # budget (the budget the leg's calls ran with, the library's automatic
+    # one included).  Beside them: the same stage-0 bytes per step of the
+    # timed region, and what the PMC counters of a profiled run of the same
+    # configuration and budget give for the same launches.
+    heavy = nd0.astype(np.int64) > budget_used
+    n_ev0 = hdr["n_ev"].astype(np.int64)
+    kern = {"stage0": {"kernel": "compact_search<Bank, G32> (stage 0)", "ms": roof_s0,
+                       "alg_bytes_per_launch": alg_bytes(hdr, np.minimum(nd0, budget_used)),
+                       "hbm_io_bytes_per_launch": hbm_bytes(hdr)}}
+    if len(roof_hv) and (roof_hv >= 0).all():
+        kern["heavy"] = {"kernel": "memo_search<Bank> (heavy stage, lane mode)", "ms": roof_hv,
+                         "heavy_histories": int(heavy.sum()),
+                         "alg_bytes_per_launch": int((32 + 8 * n_ev0[heavy]).sum() +
+                                                     16 * (nd0[heavy].astype(np.int64) - budget_used).sum())}
+    pmc = {}
     if os.path.exists(args.pmc):
         with open(args.pmc) as f:
             pmc = json.load(f)
-        if pmc.get("config") == args.config and pmc.get("n_hist") == n:
-            tr = pmc.get("hbm_bytes_per_launch")
-            roof["traffic"] = tr
-            if tr:
-                roof["hbm_actual"] = tr / t_s0 / (HBM_PEAK_GBS * 1e9)
-            valu = pmc.get("valu_insts_per_launch")
-            if valu:
-                roof["valu_issue"] = valu * VALU_CYCLES / (SIMDS * CLOCK_HZ * t_s0)
-            roof["pmc_source"] = os.path.relpath(args.pmc, ROOT)
+        if not (pmc.get("config") == args.config and pmc.get("n_hist") == n and
+                pmc.get("stage0_budget") == budget_used):
+            pmc = {}                      # measured on another configuration or budget: not this run's
+    for name, k in kern.items():
+        ms = k.pop("ms")
+        t = float(np.mean(ms)) * 1e-3
+        k["achieved"] = k["alg_bytes_per_launch"] / t / 1e9
+        k["frac"] = k["achieved"] / HBM_PEAK_GBS
+        k["kernel_ms"] = {"mean": float(np.mean(ms)), "median": float(np.median(ms)), "min": float(np.min(ms)),
+                          "launches": int(len(ms))}
+        blk = pmc if name == "stage0" else pmc.get("heavy", {})
+        k["traffic"] = blk.get("hbm_bytes_per_launch") if pmc else None
+        if k["traffic"]:
+            k["hbm_actual"] = k["traffic"] / t / (HBM_PEAK_GBS * 1e9)
+        valu = blk.get("valu_insts_per_launch") if pmc else None
+        if valu:
+            k["valu_issue"] = valu * VALU_CYCLES / (SIMDS * CLOCK_HZ * t)
+    dom = max(kern, key=lambda k: kern[k]["kernel_ms"]["mean"])
+    a_bytes = kern["stage0"]["alg_bytes_per_launch"]
+    roof = {"bound": "hbm", "achieved": kern[dom]["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": kern[dom]["frac"], "traffic": kern[dom]["traffic"], "kernel": kern[dom]["kernel"],
+            "alg_bytes_per_launch": kern[dom]["alg_bytes_per_launch"], "stage0_budget_used": budget_used,
+            "kernels": kern,
+            "call_ms": {"mean": float(np.mean(roof_call)), "median": float(np.median(roof_call))},
+            "how": "synchronous calls after the timed region, HIP events at each kernel's start and end",
+            "per_step": {"achieved": a_bytes / (ms_per_step * 1e-3) / 1e9,
+                         "frac": a_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "how": "stage 0's algorithmic bytes of one launch / ms_per_step (calls in flight)"}}
+    if pmc:
+        roof["pmc_source"] = os.path.relpath(args.pmc, ROOT)
 
     out = {
         "metric": METRIC, "value": value, "unit": "histories/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
-        "dtype_note": ("exact integer search: stage 0 holds invocation values in 14 bits, responses in 25, "
-                       "balances in int32; wider values go on to the int64 stages; node counts u64"),
+        "dtype_note": ("exact integer search: stage 0 holds invocation values in 9 bits (-256..255), responses "
+                       "in 25, balances in int32; wider values go on to the int64 stages; node counts u64"),
         "data": "synthetic (seeded scheduler-policy generator, include/qsmd_gen.h" +
                 (", generated on the GPU)" if args.device_gen else ")"),
         "config": {"workload": args.config, "histories_per_gpu": n,
@@ -519,6 +657,7 @@ def main():
                    "heavy_stage": ("lane mode, HBM memo tables" if S > 1 else "library default (wave mode for a "
                                    "short heavy list)") if not args.param else "knobs: " + ",".join(args.param),
                    "allreduce_every_steps": S * max(1, args.ar_rounds) if use_dist else None,
+                   "batches": args.rotate, "fold": fold,
                    "mode": "memo" if args.memo else "exhaustive"},
         "nodes_per_sec": nodes_total * args.steps / elapsed,
         "verdicts": {"checked": int(tot[0]), "linearisable": int(tot[1]),
@@ -526,19 +665,24 @@ def main():
                      "budget": int(tot[5])},
         "device_ms": {"in_flight": {"stage0_mean": float(np.mean(s0_ms)) if len(s0_ms) else None,
                                     "call_mean": float(np.mean(call_ms)) if len(call_ms) else None},
-                      "alone": {"stage0_mean": float(np.mean(roof_s0)), "call_mean": float(np.mean(roof_call))}},
+                      "alone": {"stage0_mean": float(np.mean(roof_s0)),
+                                "heavy_mean": float(np.mean(roof_hv)) if len(roof_hv) else None,
+                                "call_mean": float(np.mean(roof_call))}},
         "roofline": roof,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb, st_o, nd_o = cpu_baselines(hdr, ev, model_id, args.cpu_seconds, 2.0)
+        # the oracle over the last step's batch: the CPU baseline's timing and the check
+        hdr_l, ev_l = host_batches[last_batch]
+        cb, st_o, nd_o = cpu_baselines(hdr_l, ev_l, model_id, args.cpu_seconds, 2.0)
         cb["reference_shaped"] = reference_shaped(5.0)
         out["cpu_baseline"] = cb
         if args.memo:                        # node counts are "explored" there: verdicts only
             out["mismatches_vs_oracle"] = int((st_o != st).sum())
         else:
             out["mismatches_vs_oracle"] = int(((st_o != st) | (nd_o != nd.astype(np.uint64))).sum())
-        out["checked_vs_oracle"] = len(hdr)
+        out["checked_vs_oracle"] = len(hdr_l)
+        out["checked_batch"] = last_batch
     if rank == 0 and world == 1 and not args.no_extra:
         out["extra"] = {"configs": extra_configs(dev, S, knobs)}
     if rank == 0:

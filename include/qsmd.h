@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define QSMD_ABI_VERSION 2u
+#define QSMD_ABI_VERSION 3u
 
 /* ---------------------------------------------------------------- layout */
 
@@ -167,7 +167,10 @@ uint32_t qsmd_abi_version(void);
  * a stream other than the previous call's first waits (on the device) for
  * that call, because they share the context's device workspace.  Calls that
  * should overlap use one context each (bench.py keeps calls in flight that
- * way).  Contexts share no device state. */
+ * way).  Contexts share no device state.  The stream of a device call must
+ * stay alive until the context's next check call, qsmd_close, or a host wait
+ * of the context (qsmd_probe_read, qsmd_timed_out, a knob that reallocates):
+ * those wait for that stream, never for the whole device. */
 
 /* Check a batch held in HOST memory (the drop-in for one call per history;
  * n_hist = 1 is valid).  Buffers are copied in and out; the library keeps no
@@ -181,8 +184,8 @@ int qsmd_check_batch(qsmd_ctx* ctx, uint32_t model_id,
                      uint8_t* witness_out, qsmd_totals* totals_out);
 
 /* Same, with every buffer already resident in device memory (HBM) and work
- * enqueued on `stream` (a hipStream_t, NULL = the context's stream): four
- * kernel launches, no host round trip.  totals_dev (device, may be NULL)
+ * enqueued on `stream` (a hipStream_t, NULL = the context's stream): two to
+ * four kernel launches, no host round trip.  totals_dev (device, may be NULL)
  * receives the qsmd_totals of the batch.  Asynchronous: synchronise the
  * stream before reading outputs. */
 int qsmd_check_batch_device(qsmd_ctx* ctx, uint32_t model_id,
@@ -249,6 +252,10 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *   "memo_after"        lane mode: the memo joins a search after this many
  *                       nodes (default 32; before, the plain DFS without the
  *                       probe per node)
+ *   "fold"              lane mode: 1 (default) no stage-0w launch after a
+ *                       call that deferred nothing to it (the heavy stage
+ *                       takes what stage 0 defers on to the giant stage);
+ *                       0: every call launches it
  *   "timing_events"     1: record the per-call timing events (qsmd_timing_read,
  *                       qsmd_last_kernel_ms); 0 (default until
  *                       qsmd_timing_reset): none
@@ -266,6 +273,12 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *                       limit's phase-wait safety net: a giant combined by a
  *                       workgroup that gave up waiting is BUDGET) */
 int qsmd_set_param(qsmd_ctx* ctx, const char* name, uint64_t value);
+
+/* Read a knob ("stage0_budget": 0 while automatic, "fold", "heavy_mode",
+ * "memo_after") or "stage0_budget_last": the stage-0 budget the most recent
+ * finished check call ran with (the automatic one included; waits for the
+ * context's last call). */
+int qsmd_get_param(qsmd_ctx* ctx, const char* name, uint64_t* out);
 
 /* Tuning knob (default 1024): histories the compact stages cannot hold go to
  * the giant stage, which first searches each one in a lane for 16 x this
@@ -397,6 +410,11 @@ int qsmd_last_kernel_ms(qsmd_ctx* ctx, float* ms_out);
 int qsmd_timing_reset(qsmd_ctx* ctx);
 int qsmd_timing_read(qsmd_ctx* ctx, float* stage0_ms, float* call_ms, uint64_t max,
                      uint64_t* n_out);
+/* The same with heavy_ms[i] = the heavy-stage kernel of call i in lane mode
+ * (events the launch records at its start and end; -1 in wave mode).  Any of
+ * the three arrays may be NULL. */
+int qsmd_timing_read_stages(qsmd_ctx* ctx, float* stage0_ms, float* heavy_ms, float* call_ms,
+                            uint64_t max, uint64_t* n_out);
 
 /* Diagnostic: out4 = [histories stage 0 passed to stage 0w, heavy histories
  * of stage 0, heavy histories of stage 0w, giants] of the most recent check

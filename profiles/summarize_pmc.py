@@ -1,16 +1,20 @@
 """Summarise a profiles/profile.sh run: per-dispatch durations (kernel trace)
-and PMC counters of the dominant search kernel (stage 0), over the LAST
-`--last` dispatches of that kernel -- bench.py's roofline leg, the
-synchronous calls it times after its timed region -- so that the profile's
-mean duration is the one bench.py's `roofline.kernel_ms.mean` divides by.
-The whole-run rocprofv3 --stats table is kept beside it (`kernels`; its
-means include the launches that ran beside other calls in flight), and every
-kernel's stats over the roofline leg alone (`roofline_leg_kernels`).
+and PMC counters of the two search kernels that bound a call -- stage 0
+(compact_search<..., G32>) and the lane-mode heavy stage (memo_search) --
+over the LAST `--last` dispatches of each: bench.py's roofline leg, the
+synchronous calls it times after its timed region, so that the profile's
+mean durations are the ones bench.py's `roofline.kernels.*.kernel_ms.mean`
+divide by.  The whole-run rocprofv3 --stats table is kept beside it
+(`kernels`; its means include the launches that ran beside other calls in
+flight), and every kernel's stats over the roofline leg alone
+(`roofline_leg_kernels`).
 
 HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are
 collected in separate passes, are in KiB, and on gfx950 FETCH_SIZE reports
 half the bytes of a wide coalesced read, so traffic = (2*FETCH_SIZE +
 WRITE_SIZE) * 1024 per dispatch (the uncorrected value is reported too).
+(The heavy stage's reads are per-lane gathers, not wide coalesced ones; its
+block reports both.)
 
     python3 profiles/summarize_pmc.py <out_dir> [--last 30]
 """
@@ -25,6 +29,7 @@ from collections import defaultdict
 
 DOMINANT = "compact_search"
 GEOMETRY = "G32>"            # stage 0 (stage 0w is the G64 instance)
+HEAVY = "memo_search"        # the heavy stage in lane mode
 
 
 def rows(path_glob):
@@ -39,14 +44,18 @@ def is_dominant(name):
     return DOMINANT in name and GEOMETRY in name
 
 
+def is_heavy(name):
+    return HEAVY in name
+
+
 def dispatch_key(r):
     d = r.get("Dispatch_Id") or r.get("Correlation_Id") or "0"
     return int(d)
 
 
-def durations(out_dir, last):
-    """Durations (ns) of the dominant kernel's dispatches, in dispatch order."""
-    tr = [r for r in rows(os.path.join(out_dir, "trace", "**", "*kernel_trace.csv")) if is_dominant(r["Kernel_Name"])]
+def durations(out_dir, last, pick=is_dominant):
+    """Durations (ns) of a kernel's dispatches, in dispatch order."""
+    tr = [r for r in rows(os.path.join(out_dir, "trace", "**", "*kernel_trace.csv")) if pick(r["Kernel_Name"])]
     tr.sort(key=dispatch_key)
     d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr]
     return d, d[-last:] if last else d
@@ -69,10 +78,10 @@ def leg_kernels(out_dir, last):
                 "min_ns": min(v), "max_ns": max(v)} for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]))}
 
 
-def counters(out_dir, name, last):
+def counters(out_dir, name, last, pick=is_dominant):
     per = defaultdict(lambda: defaultdict(float))   # dispatch -> counter -> value
     for r in rows(os.path.join(out_dir, name, "**", "*counter_collection.csv")):
-        if not is_dominant(r.get("Kernel_Name", "")):
+        if not pick(r.get("Kernel_Name", "")):
             continue
         per[dispatch_key(r)][r["Counter_Name"]] += float(r["Counter_Value"])
     if not per:
@@ -120,16 +129,39 @@ def main():
         res["wait_any_frac"] = sq.get("SQ_WAIT_ANY", 0) / wc
         res["wait_inst_any_frac"] = sq.get("SQ_WAIT_INST_ANY", 0) / wc
         res["active_inst_frac"] = sq.get("SQ_ACTIVE_INST_ANY", 0) / wc
+    # the heavy stage: the same per-dispatch figures for memo_search
+    _, hd = durations(out_dir, args.last, is_heavy)
+    hv = {}
+    if hd:
+        hv = {"kernel": "memo_search (heavy stage, lane mode)", "dispatches": len(hd),
+              "mean_ns": statistics.mean(hd), "median_ns": statistics.median(hd), "min_ns": min(hd),
+              "max_ns": max(hd)}
+        hf, _ = counters(out_dir, "fetch", args.last, is_heavy)
+        hw, _ = counters(out_dir, "write", args.last, is_heavy)
+        hf, hw = hf.get("FETCH_SIZE"), hw.get("WRITE_SIZE")
+        hv["FETCH_SIZE_kib"], hv["WRITE_SIZE_kib"] = hf, hw
+        if hf is not None and hw is not None:
+            hv["hbm_bytes_per_launch"] = (2.0 * hf + hw) * 1024.0
+            hv["hbm_bytes_per_launch_uncorrected"] = (hf + hw) * 1024.0
+        hsq, _ = counters(out_dir, "sq1", args.last, is_heavy)
+        hsq2, _ = counters(out_dir, "sq2", args.last, is_heavy)
+        hsq.update(hsq2)
+        hv["sq"] = hsq
+        hv["valu_insts_per_launch"] = hsq.get("SQ_INSTS_VALU")
+    res["heavy"] = hv
     try:
         with open(os.path.join(out_dir, "trace.json")) as fjs:
             b = json.loads(fjs.read().strip().splitlines()[-1])
         res["config"] = b["config"]["workload"]
         res["n_hist"] = b["config"]["histories_per_gpu"]
-        res["bench_kernel_ms"] = b["roofline"].get("kernel_ms")
-        res["bench_frac"] = b["roofline"]["frac"]
-        res["bench_alg_bytes_per_launch"] = b["roofline"]["alg_bytes_per_launch"]
+        res["stage0_budget"] = b["roofline"].get("stage0_budget_used")
+        res["fold"] = b["config"].get("fold")
+        ks = b["roofline"]["kernels"]
+        res["bench_kernels"] = ks
         if d:
-            res["frac_from_profile"] = b["roofline"]["alg_bytes_per_launch"] / (res["dominant_mean_ns"] * 1e-9) / 8e12
+            res["frac_from_profile"] = ks["stage0"]["alg_bytes_per_launch"] / (res["dominant_mean_ns"] * 1e-9) / 8e12
+        if hd and ks.get("heavy"):
+            hv["frac_from_profile"] = ks["heavy"]["alg_bytes_per_launch"] / (hv["mean_ns"] * 1e-9) / 8e12
     except Exception:
         pass
     print(json.dumps(res, indent=1))

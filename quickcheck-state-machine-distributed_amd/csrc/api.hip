@@ -22,6 +22,10 @@
 
 #include "internal.h"
 #include "qsmd_gen.h"
+
+#ifndef QSMD_DIAG_FOLD2
+#define QSMD_DIAG_FOLD2 0
+#endif
 #include "qsmd.h"
 
 using namespace qsmd;
@@ -59,10 +63,11 @@ struct qsmd_ctx {
     bool in_flight = false;
     bool any_call = false;             // a check call was enqueued
     bool probe_valid = false;          // a check call finished: probe_host holds real counts
-    // timing: per call, events before stage 0, after stage 0 and after the
-    // giant stage, recorded on the launch stream (a ring of kTimingSlots)
-    std::vector<hipEvent_t> ev;        // 3 per slot
-    std::vector<uint8_t> ev_no0;       // per slot: stage 0 skipped (its end event not recorded)
+    // timing: per call, events at stage 0's start and end, after the last
+    // launch, and at the heavy stage's start and end, recorded on the launch
+    // stream (a ring of kTimingSlots)
+    std::vector<hipEvent_t> ev;        // kSlotEvents per slot
+    std::vector<uint8_t> ev_no0;       // per slot: 1 stage 0 skipped (its end event not recorded), 2 no heavy events
     uint64_t n_calls = 0;              // calls recorded since the last reset
     bool timed = false;
     // the per-call timing events above are recorded (from qsmd_timing_reset
@@ -100,6 +105,14 @@ struct qsmd_ctx {
     // 0 / 1 forces wave / lane mode, 2 (default) picks
     uint64_t heavy_mode = 2;
     uint64_t wave_max = 16384;
+    // lane mode's folded tail (memo.hip): a call whose predecessor deferred
+    // nothing to stage 0w and had no giants launches stage 0 and the heavy
+    // stage only -- the heavy stage's last workgroup finishes the call.  With
+    // calls in flight each launch of a call's chain waits for dispatch behind
+    // the other streams' stage 0 (round 4's trace: the empty stage 0w 25 us and
+    // the giant stage's short path 17 us per call on average, 4 us alone).
+    // 0 = never; the library stops folding once a folded call meets giants
+    uint64_t fold = 1;
     uint32_t* probe_host = nullptr;    // pinned: [defer, heavy32, heavy64, giant, timed] of the last finished call
     uint32_t* debug_host = nullptr;    // QSMD_SYNC_STAGES: giant-stage heartbeat (pinned)
     // lane mode's tables: one per lane slot of the memo grid
@@ -134,6 +147,7 @@ namespace {
 constexpr uint32_t kStage0wGrid = 1024;
 constexpr size_t kZeroCopyBytes = 64 * 1024;   // host calls this small run on a mapped host buffer
 constexpr uint64_t kTimingSlots = 1024;
+constexpr uint64_t kSlotEvents = 5;      // stage 0 start / end, call end, heavy start / end
 constexpr uint64_t kXMemoEntries = 1ull << 22;   // giant stage exact memo: 512 MB (shared by all giants of a call)
 constexpr uint32_t kTaskCap = 1u << 19;  // tasks per variant per call (beyond: searched unsplit)
 constexpr uint32_t kSplitTarget = 256;   // tasks wanted per giant history
@@ -168,26 +182,29 @@ static bool sync_stages() {
 
 size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
-// Wait until the context's previous call is done (its buffers may be in use).
-// (Without its completion event -- one stream so far -- the whole device: the
-// caller's stream may be gone by now.)
+// Wait until the context's previous call is done (its buffers may be in use):
+// its completion event, or (one stream so far, no event recorded) that
+// stream -- never the whole device, which would wait for other contexts,
+// torch kernels and RCCL's streams too.  The stream of a device call must
+// therefore stay alive until the context's next call, qsmd_close, or a host
+// wait of this context (include/qsmd.h).
 void quiesce(qsmd_ctx* c) {
     if (c->in_flight) {
         if (c->done_last) (void)hipEventSynchronize(c->done_ev);
-        else (void)hipDeviceSynchronize();
+        else (void)hipStreamSynchronize(c->last_stream);
         c->in_flight = false;
     }
 }
 
 // A call on stream s: the previous call of this context (on another
 // stream) comes first -- its completion event, or, the first time a second
-// stream shows up (no event recorded yet), the device; every call records
-// the event from then on.
+// stream shows up (no event recorded yet), a host wait for the previous
+// stream; every call records the event from then on.
 static hipError_t order_after_previous(qsmd_ctx* c, hipStream_t s) {
     if (!c->in_flight || c->last_stream == s) return hipSuccess;
     c->multi = true;
     if (c->done_last) return hipStreamWaitEvent(s, c->done_ev, 0);
-    const hipError_t e = hipDeviceSynchronize();
+    const hipError_t e = hipStreamSynchronize(c->last_stream);
     if (e == hipSuccess) c->in_flight = false;
     return e;
 }
@@ -289,7 +306,7 @@ int qsmd_open(qsmd_ctx** out, int device) {
         delete c;
         return QSMD_ERR_DEVICE;
     }
-    c->ev.resize(3 * kTimingSlots, nullptr);
+    c->ev.resize(kSlotEvents * kTimingSlots, nullptr);
     c->ev_no0.assign(kTimingSlots, 0);
     for (auto& e : c->ev) {
         if (hipEventCreate(&e) != hipSuccess) { qsmd_close(c); return QSMD_ERR_DEVICE; }
@@ -411,6 +428,10 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "memo_lds") {
         if (value > 2) return fail(c, QSMD_ERR_ARG, "memo_lds: 0 = HBM tables, 1 = LDS for short lists, 2 = LDS");
         c->memo_lds = (uint32_t)value;
+    } else if (n == "fold") {
+        if (value > (QSMD_DIAG_FOLD2 ? 2u : 1u))
+            return fail(c, QSMD_ERR_ARG, "fold: 0 or 1 (no stage-0w launch; 2, no giant launch either: diagnostic builds)");
+        c->fold = value;
     } else if (n == "heavy_mode") {
         if (value > 2) return fail(c, QSMD_ERR_ARG, "heavy_mode: 0 = wave, 1 = lane, 2 = auto");
         c->heavy_mode = value;
@@ -520,6 +541,33 @@ static bool lane_tables(qsmd_ctx* c, hipStream_t s, uint64_t grid) {
     return true;
 }
 
+// QSMD_SYNC_STAGES=1 (diagnostic): the giant stage's per-workgroup phase
+// records (pinned, mapped) and a heartbeat on stderr while it runs
+static uint32_t* giant_debug_buffer(qsmd_ctx* c, uint64_t gg) {
+    if (!c->debug_host)
+        (void)hipHostMalloc(reinterpret_cast<void**>(&c->debug_host), 65536 * 16,
+                            hipHostMallocMapped | hipHostMallocCoherent);
+    if (c->debug_host) std::memset(c->debug_host, 0, gg * 16);
+    return c->debug_host;
+}
+
+static void giant_heartbeat(qsmd_ctx* c, hipStream_t s, uint64_t gg) {
+    if (!c->debug_host) return;
+    for (int it = 0; hipStreamQuery(s) == hipErrorNotReady && it <= 150; ++it) {
+        usleep(200000);
+        uint32_t hist[8] = {};
+        uint64_t took = 0;
+        for (uint64_t b = 0; b < gg; ++b) {
+            const uint32_t ph = c->debug_host[b * 4];
+            hist[ph < 8 ? ph : 7]++;
+            took += c->debug_host[b * 4 + 2];
+        }
+        std::fprintf(stderr, "[qsmd] giants t=%.1fs phases 0:%u 1:%u 2:%u 3:%u 4:%u 5:%u 6:%u took %llu\n",
+                     0.2 * (it + 1), hist[0], hist[1], hist[2], hist[3], hist[4], hist[5], hist[6],
+                     (unsigned long long)took);
+    }
+}
+
 // route (known only to the host entry, which sees the headers): kSkip0 = no
 // history fits stage 0, kSkip0w = none fits stage 0w either (every history
 // goes straight to the wide list: one wave-mode launch and the giant stage)
@@ -547,8 +595,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // block sets the probe's written flag)
     if (!c->probe_valid && c->any_call && __atomic_load_n(&c->probe_host[kProbeWritten], __ATOMIC_ACQUIRE))
         c->probe_valid = true;
-    uint32_t hint[8];
-    for (int i = 0; i < 8; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
+    uint32_t hint[10];
+    for (int i = 0; i < 10; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
     const uint64_t budget0 = stage0_budget_of(c, hint);
     // the automatic budget just went down: the last call's heavy count (at
     // the higher budget) undercounts this one's -- size the tail for a long
@@ -577,6 +625,15 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
                                                                   heavy_hint + heavy_hint / 4)
                                                       : (uint64_t)c->n_cu);   // (no hint: grid-stride)
     if (lane && !(lt && !wide)) lane = lane_tables(c, s, mg);
+    // the folded tail (lane mode, ctx.fold): the last call deferred nothing
+    // to stage 0w and had a normal route -- no stage-0w launch (fold0w); and
+    // with fold 2, when it had no giants either and this call has no early
+    // exit, no giant launch (fold).  A folded call that met giants anyway
+    // (the heavy stage's solo fallback, slow) turns fold 2 off for the context
+    const bool fold0w = lane && c->fold >= 1 && c->probe_valid && route == 0u && !sync_stages() &&
+                        hint[0] == 0u && hint[2] == 0u;
+    const bool fold = fold0w && c->fold >= 2 && !early && hint[3] == 0u && hint[kProbeFold] == 0u;
+    if (c->probe_valid && hint[kProbeFold] != 0u && c->fold >= 2) c->fold = 1;
 
     // ---- workspace: header, lists, giant records, tasks
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
@@ -633,112 +690,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a.giant_count = cnt + C_GIANT;
     const bool split = c->split_budget && (!max_nodes || c->split_budget < max_nodes);
 
-    c->ws_dirty = true;                 // until the giant stage is enqueued
-    hipEvent_t* evs = &c->ev[3 * (c->n_calls % kTimingSlots)];
-    const bool tm = c->timing;
-    // ---- stage 0: every history, <= 32 events
-    SearchArgs a0 = a;
-    a0.list = nullptr;
-    a0.list_count = nullptr;
-    a0.defer_list = l0;
-    a0.defer_count = cnt + C_DEFER;
-    a0.heavy_list = h32;
-    a0.heavy_count = shards;
-    a0.heavy_shard_cap = (uint32_t)cap32;
-    a0.heavy_state = states;                 // (lane mode goes on from them)
-    a0.stage0_budget = budget0 ? budget0 : ~0ull;
-    a0.stamps = c->s0_stamps;
-    const uint64_t n_groups = std::max<uint64_t>((n_hist + 63) / 64, 1);
-    stage_done("start", s, cnt);
-    if (!(route & kSkip0)) {           // (the events at the kernel's start and end)
-        HIP_TRY(c, launch_compact(a0, (uint32_t)std::min<uint64_t>(n_groups, c->stage0_max_grid), s,
-                                  tm ? evs[0] : nullptr, tm ? evs[1] : nullptr),
-                "stage 0 launch");
-    } else if (tm) {                   // (no stage-0 end event: one packet less before the first kernel)
-        HIP_TRY(c, hipEventRecord(evs[0], s), "hipEventRecord");
-    }
-    if (tm) c->ev_no0[c->n_calls % kTimingSlots] = (route & kSkip0) ? 1u : 0u;
-    stage_done("stage0", s, cnt);
-    // ---- stage 0w: the rest, <= 64 events (beyond: the giant stage)
-    SearchArgs aw = a;
-    aw.list = (route & kSkip0) ? nullptr : l0;               // (null: every history of the batch)
-    aw.list_count = (route & kSkip0) ? nullptr : cnt + C_DEFER;
-    aw.defer_list = lw;                      // (wave mode searches most of them; the rest: giants)
-    aw.defer_count = cnt + C_WIDE;
-    aw.heavy_list = h64;
-    aw.heavy_count = cnt + C_HEAVY64;
-    aw.stage0_budget = c->stage0w_budget ? c->stage0w_budget : ~0ull;
-    if (!(route & kSkip0w))
-        HIP_TRY(c, launch_compact64(aw, (uint32_t)((route & kSkip0) ? std::min<uint64_t>(n_groups, kStage0wGrid)
-                                                                    : (hint[0] == 0u ? 8u   // (last call: none)
-                                                                                     : tail_grid(2ull * c->n_cu, kStage0wGrid,
-                                                                                                 hint[0]))),
-                                    s), "stage 0w launch");
-    stage_done("stage0w", s, cnt);
-    // ---- heavy stage: histories over the stage budgets
-    const uint64_t cap = split ? 64 * c->split_budget : 0;
-    if (lane) {
-        if (((++c->mt_epoch) & 0xFFFFFFu) == 0u && c->mt) {   // 24-bit tags wrapped: clear
-            HIP_TRY(c, hipMemsetAsync(c->mt, 0, c->mt_bytes, s), "memset memo tables");
-            ++c->mt_epoch;
-        }
-        const uint64_t slots = mg * 64 * c->mt_entries;
-        MemoArgs mp[2]{};
-        for (int w = 0; w < 2; ++w) {
-            mp[w].s = a;
-            mp[w].s.list = w ? h64 : h32;
-            mp[w].s.list_count = w ? cnt + C_HEAVY64 : shards;
-            mp[w].s.list_shard_cap = w ? 0u : (uint32_t)cap32;
-            mp[w].table = reinterpret_cast<uint32_t*>(c->mt + (w ? slots * 32 : 0));
-            mp[w].entries = (uint32_t)c->mt_entries;
-            mp[w].memo_after = (uint32_t)std::min<uint64_t>(c->memo_after, 0xFFFFFFFFull);
-            mp[w].resume = w ? nullptr : states;
-            mp[w].lds_entries = lds_entries;
-            mp[w].epoch = c->mt_epoch;
-            mp[w].giant_cap = cap;
-            mp[w].stats = c->memo_stats;
-            mp[w].stats_groups = c->memo_stats ? c->memo_stats_groups : 0;
-            mp[w].fwd_list = lw;                 // stage 0w's deferred histories: on to the giant stage
-            mp[w].fwd_count = cnt + C_WIDE;
-        }
-        HIP_TRY(c, launch_memo(mp[0], mp[1], (uint32_t)mg, wide, lt, s), "memo launch");
-        stage_done("lane", s, cnt);
-    } else {
-        WaveArgs wp{};
-        wp.s = a;
-        wp.list32 = h32;
-        wp.count32 = shards;
-        wp.cap32 = (uint32_t)cap32;
-        wp.list64 = h64;
-        wp.count64 = cnt + C_HEAVY64;
-        wp.list_wide = (route & kSkip0w) ? nullptr : lw;
-        wp.count_wide = cnt + C_WIDE;
-        wp.explore_cap = cap;
-        wp.explore_cap_wide = split ? 16 * c->split_budget : 0;   // (the giant stage's whole-search cap)
-        wp.stats = c->wave_stats;
-        wp.memo_min_rem = (uint32_t)c->wave_min_rem;
-        wp.dag_states = (uint32_t)(c->dag_states & ~1ull);   // (even: the DAG's LDS arrays stay 8-B aligned)
-        wp.dag_items = 4u * wp.dag_states;
-        wp.dbg = c->dag_dbg;
-        wp.dbg_h = (uint32_t)c->dag_dbg_h;
-        wp.memo_mode = (flags & QSMD_FLAG_MEMO) ? 1u : 0u;
-        // LDS memo table: 8 KB per wavefront (256 entries of <= 64 events),
-        // 64 KB when the last call had wide histories (1024 entries of <= 128)
-        const uint64_t wide_hint = (route & kSkip0w) ? n_hist : (c->probe_valid ? (uint64_t)hint[kProbeWide] : 0ull);
-        wp.buckets = wide_hint ? 256u : 32u;
-        // one workgroup per history the last call sent here (+ 25 %), at
-        // least 64 and at most 16 per CU (grid-stride beyond)
-        // the 65..128-event launch when the last call had wide histories
-        wp.wide128 = wide_hint ? 1u : 0u;
-        const uint64_t nh = heavy_hint + wide_hint;
-        const uint64_t g = c->wave_grid ? c->wave_grid
-                         : std::min<uint64_t>(16ull * c->n_cu,
-                                              c->probe_valid ? std::max<uint64_t>(64, nh + nh / 4) : 4ull * c->n_cu);
-        const uint64_t g128 = std::min<uint64_t>(16ull * c->n_cu, std::max<uint64_t>(8, wide_hint + wide_hint / 4));
-        HIP_TRY(c, launch_wave(wp, (route & kSkip0w) ? 0u : (uint32_t)g, (uint32_t)g128, s), "wave launch");
-        stage_done("wave", s, cnt);
-    }
-    // ---- giant stage: the split search, the combine, (the fixup), the totals
+    // ---- the giant stage's arguments (its launch, or the folded tail's last
+    // workgroup: the split search, the combine, (the fixup), the totals)
     SplitArgs p{};
     p.s = a;
     p.cnt = cnt;
@@ -780,32 +733,118 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         p.memo_exact = 1;
         p.memo_epoch = c->xm_epoch;
     }
-    const uint64_t gg = c->giant_grid ? c->giant_grid
-                                      : (early || hint[3] ? 2ull * c->n_cu : 64ull);
-    if (sync_stages()) {
-        if (!c->debug_host)
-            (void)hipHostMalloc(reinterpret_cast<void**>(&c->debug_host), 65536 * 16, hipHostMallocMapped | hipHostMallocCoherent);
-        std::memset(c->debug_host, 0, gg * 16);
-        p.debug = c->debug_host;
+    c->ws_dirty = true;                 // until the giant stage is enqueued
+    hipEvent_t* evs = &c->ev[kSlotEvents * (c->n_calls % kTimingSlots)];
+    const bool tm = c->timing;
+    // ---- stage 0: every history, <= 32 events
+    SearchArgs a0 = a;
+    a0.list = nullptr;
+    a0.list_count = nullptr;
+    a0.defer_list = l0;
+    a0.defer_count = cnt + C_DEFER;
+    a0.heavy_list = h32;
+    a0.heavy_count = shards;
+    a0.heavy_shard_cap = (uint32_t)cap32;
+    a0.heavy_state = states;                 // (lane mode goes on from them)
+    a0.stage0_budget = budget0 ? budget0 : ~0ull;
+    a0.stamps = c->s0_stamps;
+    const uint64_t n_groups = std::max<uint64_t>((n_hist + 63) / 64, 1);
+    stage_done("start", s, cnt);
+    if (!(route & kSkip0)) {           // (the events at the kernel's start and end)
+        HIP_TRY(c, launch_compact(a0, (uint32_t)std::min<uint64_t>(n_groups, c->stage0_max_grid), s,
+                                  tm ? evs[0] : nullptr, tm ? evs[1] : nullptr),
+                "stage 0 launch");
+    } else if (tm) {                   // (no stage-0 end event: one packet less before the first kernel)
+        HIP_TRY(c, hipEventRecord(evs[0], s), "hipEventRecord");
     }
-    HIP_TRY(c, launch_giants(p, (uint32_t)gg, s), "giant launch");
-    if (sync_stages()) {                 // heartbeat while it runs
-        const uint32_t dn = p.target ? p.task_cap : 0;
-        (void)dn;
-        for (int it = 0; hipStreamQuery(s) == hipErrorNotReady; ++it) {
-            usleep(200000);
-            uint32_t hist[8] = {};
-            uint64_t took = 0;
-            for (uint64_t b = 0; b < gg; ++b) {
-                const uint32_t ph = c->debug_host[b * 4];
-                hist[ph < 8 ? ph : 7]++;
-                took += c->debug_host[b * 4 + 2];
-            }
-            std::fprintf(stderr, "[qsmd] giants t=%.1fs phases 0:%u 1:%u 2:%u 3:%u 4:%u 5:%u 6:%u took %llu\n",
-                         0.2 * (it + 1), hist[0], hist[1], hist[2], hist[3], hist[4], hist[5], hist[6],
-                         (unsigned long long)took);
-            if (it > 150) break;
+    if (tm) c->ev_no0[c->n_calls % kTimingSlots] = ((route & kSkip0) ? 1u : 0u) | (lane ? 0u : 2u);
+    stage_done("stage0", s, cnt);
+    // ---- stage 0w: the rest, <= 64 events (beyond: the giant stage)
+    SearchArgs aw = a;
+    aw.list = (route & kSkip0) ? nullptr : l0;               // (null: every history of the batch)
+    aw.list_count = (route & kSkip0) ? nullptr : cnt + C_DEFER;
+    aw.defer_list = lw;                      // (wave mode searches most of them; the rest: giants)
+    aw.defer_count = cnt + C_WIDE;
+    aw.heavy_list = h64;
+    aw.heavy_count = cnt + C_HEAVY64;
+    aw.stage0_budget = c->stage0w_budget ? c->stage0w_budget : ~0ull;
+    if (!(route & kSkip0w) && !fold0w)
+        HIP_TRY(c, launch_compact64(aw, (uint32_t)((route & kSkip0) ? std::min<uint64_t>(n_groups, kStage0wGrid)
+                                                                    : (hint[0] == 0u ? 8u   // (last call: none)
+                                                                                     : tail_grid(2ull * c->n_cu, kStage0wGrid,
+                                                                                                 hint[0]))),
+                                    s), "stage 0w launch");
+    stage_done("stage0w", s, cnt);
+    // ---- heavy stage: histories over the stage budgets
+    const uint64_t cap = split ? 64 * c->split_budget : 0;
+    if (lane) {
+        if (((++c->mt_epoch) & 0xFFFFFFu) == 0u && c->mt) {   // 24-bit tags wrapped: clear
+            HIP_TRY(c, hipMemsetAsync(c->mt, 0, c->mt_bytes, s), "memset memo tables");
+            ++c->mt_epoch;
         }
+        const uint64_t slots = mg * 64 * c->mt_entries;
+        MemoArgs mp[2]{};
+        for (int w = 0; w < 2; ++w) {
+            mp[w].s = a;
+            // (folded: no stage 0w ran, G64 groups are stage 0's deferred histories)
+            mp[w].s.list = w ? (fold0w ? l0 : h64) : h32;
+            mp[w].s.list_count = w ? cnt + (fold0w ? C_DEFER : C_HEAVY64) : shards;
+            mp[w].s.list_shard_cap = w ? 0u : (uint32_t)cap32;
+            mp[w].table = reinterpret_cast<uint32_t*>(c->mt + (w ? slots * 32 : 0));
+            mp[w].entries = (uint32_t)c->mt_entries;
+            mp[w].memo_after = (uint32_t)std::min<uint64_t>(c->memo_after, 0xFFFFFFFFull);
+            mp[w].resume = w ? nullptr : states;
+            mp[w].lds_entries = lds_entries;
+            mp[w].epoch = c->mt_epoch;
+            mp[w].giant_cap = cap;
+            mp[w].stats = c->memo_stats;
+            mp[w].stats_groups = c->memo_stats ? c->memo_stats_groups : 0;
+            mp[w].fwd_list = lw;                 // stage 0w's deferred histories: on to the giant stage
+            mp[w].fwd_count = cnt + C_WIDE;
+        }
+        HIP_TRY(c, launch_memo(mp[0], mp[1], (uint32_t)mg, wide, lt, fold, p, s, tm ? evs[3] : nullptr,
+                               tm ? evs[4] : nullptr), "memo launch");
+        stage_done("lane", s, cnt);
+    } else {
+        WaveArgs wp{};
+        wp.s = a;
+        wp.list32 = h32;
+        wp.count32 = shards;
+        wp.cap32 = (uint32_t)cap32;
+        wp.list64 = h64;
+        wp.count64 = cnt + C_HEAVY64;
+        wp.list_wide = (route & kSkip0w) ? nullptr : lw;
+        wp.count_wide = cnt + C_WIDE;
+        wp.explore_cap = cap;
+        wp.explore_cap_wide = split ? 16 * c->split_budget : 0;   // (the giant stage's whole-search cap)
+        wp.stats = c->wave_stats;
+        wp.memo_min_rem = (uint32_t)c->wave_min_rem;
+        wp.dag_states = (uint32_t)(c->dag_states & ~1ull);   // (even: the DAG's LDS arrays stay 8-B aligned)
+        wp.dag_items = 4u * wp.dag_states;
+        wp.dbg = c->dag_dbg;
+        wp.dbg_h = (uint32_t)c->dag_dbg_h;
+        wp.memo_mode = (flags & QSMD_FLAG_MEMO) ? 1u : 0u;
+        // LDS memo table: 8 KB per wavefront (256 entries of <= 64 events),
+        // 64 KB when the last call had wide histories (1024 entries of <= 128)
+        const uint64_t wide_hint = (route & kSkip0w) ? n_hist : (c->probe_valid ? (uint64_t)hint[kProbeWide] : 0ull);
+        wp.buckets = wide_hint ? 256u : 32u;
+        // one workgroup per history the last call sent here (+ 25 %), at
+        // least 64 and at most 16 per CU (grid-stride beyond)
+        // the 65..128-event launch when the last call had wide histories
+        wp.wide128 = wide_hint ? 1u : 0u;
+        const uint64_t nh = heavy_hint + wide_hint;
+        const uint64_t g = c->wave_grid ? c->wave_grid
+                         : std::min<uint64_t>(16ull * c->n_cu,
+                                              c->probe_valid ? std::max<uint64_t>(64, nh + nh / 4) : 4ull * c->n_cu);
+        const uint64_t g128 = std::min<uint64_t>(16ull * c->n_cu, std::max<uint64_t>(8, wide_hint + wide_hint / 4));
+        HIP_TRY(c, launch_wave(wp, (route & kSkip0w) ? 0u : (uint32_t)g, (uint32_t)g128, s), "wave launch");
+        stage_done("wave", s, cnt);
+    }
+    if (!fold) {
+        const uint64_t gg = c->giant_grid ? c->giant_grid : (early || hint[3] ? 2ull * c->n_cu : 64ull);
+        if (sync_stages()) p.debug = giant_debug_buffer(c, gg);
+        HIP_TRY(c, launch_giants(p, (uint32_t)gg, s), "giant launch");
+        if (sync_stages()) giant_heartbeat(c, s, gg);
     }
     stage_done("giants", s, cnt);
     c->ws_dirty = false;
@@ -1016,7 +1055,7 @@ int qsmd_wellformed_batch(qsmd_ctx* c, const qsmd_hdr* hdr, uint64_t n_hist, con
 int qsmd_last_kernel_ms(qsmd_ctx* c, float* ms) {
     if (!c || !ms) return QSMD_ERR_ARG;
     if (!c->timed || c->n_calls == 0) return fail(c, QSMD_ERR_ARG, "no timed check call yet (qsmd_timing_reset first)");
-    hipEvent_t* evs = &c->ev[3 * ((c->n_calls - 1) % kTimingSlots)];
+    hipEvent_t* evs = &c->ev[kSlotEvents * ((c->n_calls - 1) % kTimingSlots)];
     HIP_TRY(c, hipEventSynchronize(evs[2]), "hipEventSynchronize");
     HIP_TRY(c, hipEventElapsedTime(ms, evs[0], evs[2]), "hipEventElapsedTime");
     return QSMD_OK;
@@ -1030,21 +1069,54 @@ int qsmd_timing_reset(qsmd_ctx* c) {
     return QSMD_OK;
 }
 
-int qsmd_timing_read(qsmd_ctx* c, float* stage0_ms, float* call_ms, uint64_t max, uint64_t* n_out) {
+int qsmd_timing_read_stages(qsmd_ctx* c, float* stage0_ms, float* heavy_ms, float* call_ms, uint64_t max,
+                            uint64_t* n_out) {
     if (!c || !n_out) return QSMD_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
     const uint64_t n = std::min<uint64_t>(std::min<uint64_t>(c->n_calls, kTimingSlots), max);
     const uint64_t first = c->n_calls - n;
     for (uint64_t i = 0; i < n; ++i) {
-        hipEvent_t* evs = &c->ev[3 * ((first + i) % kTimingSlots)];
+        hipEvent_t* evs = &c->ev[kSlotEvents * ((first + i) % kTimingSlots)];
+        const uint8_t no = c->ev_no0[(first + i) % kTimingSlots];
         HIP_TRY(c, hipEventSynchronize(evs[2]), "hipEventSynchronize");
         if (stage0_ms) {
-            if (c->ev_no0[(first + i) % kTimingSlots]) stage0_ms[i] = 0.0f;   // (no stage 0 in that call)
+            if (no & 1u) stage0_ms[i] = 0.0f;   // (no stage 0 in that call)
             else HIP_TRY(c, hipEventElapsedTime(&stage0_ms[i], evs[0], evs[1]), "elapsed");
+        }
+        if (heavy_ms) {
+            if (no & 2u) heavy_ms[i] = -1.0f;   // (the heavy stage in wave mode: not timed)
+            else HIP_TRY(c, hipEventElapsedTime(&heavy_ms[i], evs[3], evs[4]), "elapsed");
         }
         if (call_ms) HIP_TRY(c, hipEventElapsedTime(&call_ms[i], evs[0], evs[2]), "elapsed");
     }
     *n_out = n;
+    return QSMD_OK;
+}
+
+int qsmd_timing_read(qsmd_ctx* c, float* stage0_ms, float* call_ms, uint64_t max, uint64_t* n_out) {
+    return qsmd_timing_read_stages(c, stage0_ms, nullptr, call_ms, max, n_out);
+}
+
+int qsmd_get_param(qsmd_ctx* c, const char* name, uint64_t* out) {
+    if (!c || !name || !out) return QSMD_ERR_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    const std::string n(name);
+    if (n == "stage0_budget_last") {         // the stage-0 budget of the most recent finished call
+        quiesce(c);
+        if (!__atomic_load_n(&c->probe_host[kProbeWritten], __ATOMIC_ACQUIRE))
+            return fail(c, QSMD_ERR_ARG, "stage0_budget_last: no finished check call");
+        *out = c->probe_host[kProbeBudget];
+    } else if (n == "stage0_budget") {       // the set budget, 0 while automatic
+        *out = c->s0_auto ? 0 : c->stage0_budget;
+    } else if (n == "fold") {
+        *out = c->fold;
+    } else if (n == "heavy_mode") {
+        *out = c->heavy_mode;
+    } else if (n == "memo_after") {
+        *out = c->memo_after;
+    } else {
+        return fail(c, QSMD_ERR_ARG, "unknown parameter");
+    }
     return QSMD_OK;
 }
 

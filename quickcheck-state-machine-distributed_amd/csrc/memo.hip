@@ -24,10 +24,21 @@
 // their balances as i16; Ticket: Just n).  A state outside that encoding
 // (a balance beyond i16, a count beyond u32) is simply not recorded.  One
 // writer and reader per table: plain loads and stores, no atomics.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "internal.h"
 #include "lane.h"
+#include "split.h"
+
+// QSMD_DIAG_FOLD2=1 (diagnostic builds only, tools/build_variant.sh): the
+// folded tail that also takes the giant launch's place (fold 2), without a
+// giant fallback -- the whole giant stage in this kernel would cost it its
+// register budget (248 VGPRs: occupancy 1 instead of 4), so a call with
+// giants is left unsearched there (flagged through the time-limit word)
+#ifndef QSMD_DIAG_FOLD2
+#define QSMD_DIAG_FOLD2 0
+#endif
 
 namespace qsmd {
 
@@ -44,7 +55,7 @@ struct MemoEntry {
 };
 
 template <uint32_t MODEL, class G>
-struct MemoKey {
+struct LaneKey {
     uint32_t w1, rem_lo, rem_hi, m[4];
     uint32_t slot;
     bool ok;
@@ -52,10 +63,10 @@ struct MemoKey {
 
 // the key of the lane's current state (the node at depth dfs.depth)
 template <uint32_t MODEL, class G>
-__device__ __forceinline__ MemoKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d, const SearchArgs& a,
+__device__ __forceinline__ LaneKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d, const SearchArgs& a,
                                                       int32_t (*s_bal)[C_LANES], int lane, uint32_t epoch,
                                                       uint32_t mask) {
-    MemoKey<MODEL, G> k;
+    LaneKey<MODEL, G> k;
     k.ok = true;
     k.rem_lo = (uint32_t)d.rem;
     k.rem_hi = G::EV == 64 ? (uint32_t)((uint64_t)d.rem >> 32) : 0u;
@@ -92,7 +103,7 @@ __device__ __forceinline__ MemoKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d
 }
 
 template <uint32_t MODEL, class G>
-__device__ __forceinline__ bool memo_lookup(const uint32_t* tab, const MemoKey<MODEL, G>& k, uint32_t h,
+__device__ __forceinline__ bool memo_lookup(const uint32_t* tab, const LaneKey<MODEL, G>& k, uint32_t h,
                                             uint32_t& count) {
     const uint4* e = reinterpret_cast<const uint4*>(tab + (uint64_t)k.slot * MemoEntry<G>::W);
     const uint4 x0 = e[0], x1 = e[1];
@@ -104,7 +115,7 @@ __device__ __forceinline__ bool memo_lookup(const uint32_t* tab, const MemoKey<M
 }
 
 template <uint32_t MODEL, class G>
-__device__ __forceinline__ void memo_insert(uint32_t* tab, const MemoKey<MODEL, G>& k, uint32_t h, uint32_t count) {
+__device__ __forceinline__ void memo_insert(uint32_t* tab, const LaneKey<MODEL, G>& k, uint32_t h, uint32_t count) {
     uint4* e = reinterpret_cast<uint4*>(tab + (uint64_t)k.slot * MemoEntry<G>::W);
     e[0] = make_uint4(h, k.w1, k.rem_lo, count);
     e[1] = make_uint4(k.m[0], k.m[1], k.m[2], k.m[3]);
@@ -122,7 +133,7 @@ constexpr uint32_t kNoHistory = 0xFFFFFFFFu;
 constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
 
 template <uint32_t MODEL, class G>
-__device__ __forceinline__ bool memo_lookup_lds(const uint32_t* col, const MemoKey<MODEL, G>& k, uint32_t h,
+__device__ __forceinline__ bool memo_lookup_lds(const uint32_t* col, const LaneKey<MODEL, G>& k, uint32_t h,
                                                 uint32_t& count) {
     const uint32_t* e = col + k.slot * 8u * C_LANES;
     bool hit = e[0] == h && e[1 * C_LANES] == k.w1 && e[2 * C_LANES] == k.rem_lo && e[4 * C_LANES] == k.m[0];
@@ -133,7 +144,7 @@ __device__ __forceinline__ bool memo_lookup_lds(const uint32_t* col, const MemoK
 }
 
 template <uint32_t MODEL, class G>
-__device__ __forceinline__ void memo_insert_lds(uint32_t* col, const MemoKey<MODEL, G>& k, uint32_t h, uint32_t count) {
+__device__ __forceinline__ void memo_insert_lds(uint32_t* col, const LaneKey<MODEL, G>& k, uint32_t h, uint32_t count) {
     uint32_t* e = col + k.slot * 8u * C_LANES;
     e[0] = h;
     e[1 * C_LANES] = k.w1;
@@ -170,7 +181,7 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
         // (counts kept mod 2^32: exact while the running count is below 2^32)
         if (memo && !skip && d.nodes <= 0xFFFFFFFFull && entry[(d.depth - 1u) * C_LANES] != kNoEntry) {
             const uint32_t cnt = (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES];
-            const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
+            const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             if (k.ok) {
                 if constexpr (LT) memo_insert_lds<MODEL, G>(tab, k, h, cnt);
                 else memo_insert<MODEL, G>(tab, k, h, cnt);
@@ -188,7 +199,7 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
             entry[dep0 * C_LANES] = (uint32_t)d.nodes;
         }
         if (memo && d.depth > dep0 && status < 0) {
-            const MemoKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
+            const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             uint32_t cnt = 0;
             bool hit = false;
             if (k.ok) {
@@ -344,8 +355,16 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
 // searches any history exactly from the root.  LT (never with `wide`): the
 // G32 memo tables in LDS after the group (a short list: the heavy stage's
 // time is one search's DFS chain, and the HBM probe was half of it).
+//
+// With the folded tail (api.hip fold0w: the last call deferred nothing) no
+// stage 0w runs: p64's list is stage 0's deferred list, which without `wide`
+// goes on to the giant list.  fold (diagnostic builds, QSMD_DIAG_FOLD2): the
+// launch is also the call's last -- the last workgroup out (a ticket on
+// C_MEXIT) finishes the call (totals, probe, counters) instead of the giant
+// launch.
 template <uint32_t MODEL, bool LT>
-__global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32, MemoArgs p64, uint32_t wide) {
+__global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(SplitArgs t, MemoArgs p32, MemoArgs p64,
+                                                                   uint32_t wide, uint32_t fold) {
     extern __shared__ uint32_t lds[];
     const int lane = threadIdx.x;
     const uint64_t n32 = (list_total(p32.s.list_count, p32.s.list_shard_cap) + 63u) / 64u,
@@ -381,6 +400,30 @@ __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32,
         }
     }
     cnt.flush(p32.s.buckets, lane);
+#if QSMD_DIAG_FOLD2
+    if (fold) {
+        // the last workgroup out: every other one has stored its results and
+        // counts (drained, then released with the ticket)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t last = 0;
+        if (lane == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            last = atomicAdd(t.cnt + C_MEXIT, 1u) == gridDim.x - 1u;
+        }
+        if (__shfl(last, 0, 64)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (ld_cnt(t.cnt + C_GIANT) != 0u) {
+                if (t.probe_host && lane == 0) t.probe_host[kProbeFold] = 1u;
+                if (lane == 0) atomicOr(t.s.timed_out, 4u);
+            }
+            finish_call(t, lane);
+        }
+    }
+#else
+    (void)fold;
+#endif
 }
 
 template <uint32_t MODEL>
@@ -389,10 +432,12 @@ static size_t memo_lds_bytes(uint32_t lds_entries) {
 }
 
 template <uint32_t MODEL, bool LT>
-static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s) {
+static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool fold,
+                                const SplitArgs& t, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
     const size_t lds = LT ? memo_lds_bytes<MODEL>(p32.lds_entries)
                           : (wide ? sizeof(MemoLds<MODEL, G64>) : sizeof(MemoLds<MODEL, G32>));
-    hipLaunchKernelGGL((memo_search<MODEL, LT>), dim3(grid), dim3(C_LANES), lds, s, p32, p64, wide ? 1u : 0u);
+    hipExtLaunchKernelGGL((memo_search<MODEL, LT>), dim3(grid), dim3(C_LANES), lds, s, start, stop, 0u, t, p32, p64,
+                          wide ? 1u : 0u, fold ? 1u : 0u);
     return hipGetLastError();
 }
 
@@ -417,13 +462,13 @@ bool memo_lds_accepted(uint32_t model_id, uint32_t lds_entries, size_t cap) {
 
 // lds_tables (with !wide): the caller has checked memo_lds_accepted
 hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool lds_tables,
-                       hipStream_t s) {
+                       bool fold, const SplitArgs& t, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
     const bool bank = p32.s.model_id == QSMD_MODEL_BANK;
     if (lds_tables && !wide)
-        return bank ? launch_memo_t<QSMD_MODEL_BANK, true>(p32, p64, grid, wide, s)
-                    : launch_memo_t<QSMD_MODEL_TICKET, true>(p32, p64, grid, wide, s);
-    return bank ? launch_memo_t<QSMD_MODEL_BANK, false>(p32, p64, grid, wide, s)
-                : launch_memo_t<QSMD_MODEL_TICKET, false>(p32, p64, grid, wide, s);
+        return bank ? launch_memo_t<QSMD_MODEL_BANK, true>(p32, p64, grid, wide, fold, t, s, start, stop)
+                    : launch_memo_t<QSMD_MODEL_TICKET, true>(p32, p64, grid, wide, fold, t, s, start, stop);
+    return bank ? launch_memo_t<QSMD_MODEL_BANK, false>(p32, p64, grid, wide, fold, t, s, start, stop)
+                : launch_memo_t<QSMD_MODEL_TICKET, false>(p32, p64, grid, wide, fold, t, s, start, stop);
 }
 
 }  // namespace qsmd

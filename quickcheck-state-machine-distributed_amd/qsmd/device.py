@@ -72,6 +72,8 @@ EXPORTS = {
     "qsmd_last_kernel_ms": (_I, [_P, ctypes.POINTER(ctypes.c_float)]),
     "qsmd_timing_reset": (_I, [_P]),
     "qsmd_timing_read": (_I, [_P, _P, _P, _U64, ctypes.POINTER(_U64)]),
+    "qsmd_timing_read_stages": (_I, [_P, _P, _P, _P, _U64, ctypes.POINTER(_U64)]),
+    "qsmd_get_param": (_I, [_P, ctypes.c_char_p, ctypes.POINTER(_U64)]),
     "qsmd_set_split_budget": (_I, [_P, _U64]),
     "qsmd_set_param": (_I, [_P, ctypes.c_char_p, _U64]),
     "qsmd_set_memo_capacity": (_I, [_P, _U64]),
@@ -333,12 +335,26 @@ class Context:
 
     def timing_read(self, max_calls=1024):
         """(stage0_ms, call_ms) arrays for the calls since timing_reset()."""
+        s0, _, call = self.timing_read_stages(max_calls)
+        return s0, call
+
+    def timing_read_stages(self, max_calls=1024):
+        """(stage0_ms, heavy_ms, call_ms) arrays for the calls since
+        timing_reset(); heavy_ms = the lane-mode heavy-stage kernel (-1 in
+        wave mode)."""
         s0 = np.zeros(max_calls, dtype=np.float32)
+        hv = np.zeros(max_calls, dtype=np.float32)
         call = np.zeros(max_calls, dtype=np.float32)
         n = ctypes.c_uint64()
-        self._check(self._lib.qsmd_timing_read(self._h, _ptr(s0), _ptr(call), max_calls,
-                                               ctypes.byref(n)), "qsmd_timing_read")
-        return s0[: n.value], call[: n.value]
+        self._check(self._lib.qsmd_timing_read_stages(self._h, _ptr(s0), _ptr(hv), _ptr(call), max_calls,
+                                                      ctypes.byref(n)), "qsmd_timing_read_stages")
+        return s0[: n.value], hv[: n.value], call[: n.value]
+
+    def get_param(self, name):
+        """qsmd_get_param: a knob's value, or "stage0_budget_last"."""
+        out = ctypes.c_uint64()
+        self._check(self._lib.qsmd_get_param(self._h, name.encode(), ctypes.byref(out)), f"qsmd_get_param({name})")
+        return int(out.value)
 
 
 _default = None

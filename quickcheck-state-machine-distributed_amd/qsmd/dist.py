@@ -169,6 +169,82 @@ def check_shard_early_exit(checker, model_id, hdr, events, n_total, rank, world,
     return status, nodes, dict(first_fail=best, rounds=rounds, searched=searched)
 
 
+def check_shard_early_exit_device(ctx, model_id, d_hdr, d_ev, n_events, n_total, rank, world, chunk=262144,
+                                  group=None, max_nodes=0):
+    """check_shard_early_exit on DEVICE-resident buffers (the
+    reference's parallel property stops at its first failing test,
+    /root/reference/test/TicketDispenser.hs:284-322).
+
+    d_hdr / d_ev: this rank's shard as uint8 torch tensors on its GPU (the
+    include/qsmd.h records; ev_off relative to d_ev).  Each round checks the
+    rank's next chunk in place through qsmd_check_batch_device with
+    QSMD_FLAG_EARLY_EXIT_BATCH (headers at the chunk's offset, the shard's
+    whole event buffer, outputs into the shard's status / node arrays).  The
+    chunk's first failure comes from its device totals -- with the flag every
+    history after it is SKIPPED, so it is the chunk's last history minus the
+    skipped count -- and one MIN all-reduce per round (RCCL on a device
+    tensor under nccl) publishes the global first failure; its 8-byte result
+    is the only value that reaches the host per round, for the decision to
+    stop.  Status and node arrays stay on the device.  Everything runs on the
+    current torch stream.  Same rounds, stopping
+    rule and final SKIPPED marking as the host version, so status, nodes and
+    totals equal one context's early exit over the concatenated batch.
+
+    Returns (status u8 tensor, nodes i64 tensor, info) for this rank's shard;
+    info: first_fail (n_total if none), rounds, searched (histories the
+    device did not skip), totals (this rank's, int64[8] tensor on the
+    device) -- all-reduce them with allreduce_totals for the batch's."""
+    import torch
+    import torch.distributed as dist
+
+    from . import device
+
+    first, count = shard(n_total, rank, world)
+    dev = d_hdr.device
+    status = torch.full((count,), 5, dtype=torch.uint8, device=dev)     # SKIPPED until searched
+    nodes = torch.zeros(count, dtype=torch.int64, device=dev)
+    starts = [shard(n_total, r, world) for r in range(world)]
+    rounds_all = max((c + chunk - 1) // chunk for _, c in starts) if n_total else 0
+    tot = torch.zeros((max(rounds_all, 1), 8), dtype=torch.int64, device=dev)
+    local = torch.full((1,), n_total, dtype=torch.int64, device=dev)
+    searched = torch.zeros((), dtype=torch.int64, device=dev)
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    cdev = _collective_device(group) if multi else dev
+    s = torch.cuda.current_stream(dev).cuda_stream          # the calls and the torch ops below: one stream
+    flags = device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_EARLY_EXIT_BATCH
+    best, rounds = n_total, 0
+    for k in range(rounds_all):
+        if not any(k * chunk < c and f + k * chunk < best for f, c in starts):
+            break
+        a = k * chunk
+        if a < count and first + a < best:
+            b = min(count, a + chunk)
+            ctx.check_device(model_id, d_hdr.data_ptr() + 16 * a, b - a, d_ev.data_ptr(), n_events,
+                             status.data_ptr() + a, nodes.data_ptr() + 8 * a, None, tot[k].data_ptr(),
+                             flags=flags, max_nodes=max_nodes, stream=s)
+            t = tot[k]
+            ff = (first + b - 1) - t[6]                        # the chunk's first failure, if it has one
+            local = torch.where((t[2] + t[3]) > 0, torch.minimum(local, ff), local)
+            searched += (b - a) - t[6]
+        r = local.to(cdev)
+        if multi:
+            dist.all_reduce(r, op=dist.ReduceOp.MIN, group=group)
+        best = int(r.item())
+        local.fill_(best)
+        rounds += 1
+    cut = best - first                                         # local index of the global first failure
+    if cut < count:
+        after = max(0, cut + 1)
+        status[after:] = 5
+        nodes[after:] = 0
+    t = torch.zeros(8, dtype=torch.int64, device=dev)
+    bc = torch.bincount(status.to(torch.int64), minlength=6)
+    t[1], t[2], t[3], t[4], t[5], t[6] = bc[1], bc[0], bc[2], bc[3], bc[4], bc[5]
+    t[0] = bc[0] + bc[1] + bc[2]
+    t[7] = nodes.sum()
+    return status, nodes, dict(first_fail=best, rounds=rounds, searched=int(searched.item()), totals=t)
+
+
 def device_checker(ctx, max_nodes=0):
     """Checker running the HIP search through the C ABI (host buffers);
     early=True adds QSMD_FLAG_EARLY_EXIT_BATCH."""

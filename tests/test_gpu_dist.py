@@ -95,12 +95,19 @@ def _worker(rank, world, port, n_total, out_q):
             h, e = qdist.chunk_slice(hdr, ev, first, first + count)
             st, nd, info = qdist.check_shard_early_exit(qdist.device_checker(ctx, max_nodes=10**7), mid, h, e,
                                                         n_total, rank, world, chunk=2048)
+            # the same on device-resident buffers (one MIN all-reduce per chunk, statuses stay on the GPU)
+            d_h = torch.from_numpy(h.view(np.uint8)).cuda()
+            d_e = torch.from_numpy(e.view(np.uint8)).cuda()
+            dst, dnd, dinfo = qdist.check_shard_early_exit_device(ctx, mid, d_h, d_e, len(e), n_total, rank, world,
+                                                                  chunk=2048, max_nodes=10**7)
+            dtot, _ = qdist.allreduce_totals(dinfo.pop("totals"))
+            dev_res = (dst.cpu().tolist(), dnd.cpu().tolist(), dinfo, dtot.tolist())
             one = None
             if rank == 0:
                 st1, nd1, _, tot1 = ctx.check_arrays(mid, hdr, ev, max_nodes=10**7, flags=device.QSMD_FLAG_EXHAUSTIVE |
                                                      device.QSMD_FLAG_EARLY_EXIT_BATCH)
                 one = (st1.tolist(), [int(x) for x in nd1], tot1)
-            ee.append((st.tolist(), [int(x) for x in nd], info, one))
+            ee.append((st.tolist(), [int(x) for x in nd], info, one, dev_res))
         res["early"] = ee
         out_q.put((rank, res))
     finally:
@@ -181,3 +188,15 @@ def test_two_processes_on_the_hip_kernels():
         assert ff == results[1]["early"][j][2]["first_fail"] < n_total
         searched = results[0]["early"][j][2]["searched"] + results[1]["early"][j][2]["searched"]
         assert ff + 1 <= searched < n_total, (config, plant, searched)
+        # the device-resident path: status for status, count for count the same,
+        # the same rounds and histories searched, the all-reduced totals the batch's
+        dev_st = np.array(results[0]["early"][j][4][0] + results[1]["early"][j][4][0], dtype=np.uint8)
+        dev_nd = np.array(results[0]["early"][j][4][1] + results[1]["early"][j][4][1], dtype=np.uint64)
+        assert np.array_equal(dev_st, np.array(st1, dtype=np.uint8)), config
+        assert np.array_equal(dev_nd, np.array(nd1, dtype=np.uint64)), config
+        for r in range(world):
+            dinfo, dtot = results[r]["early"][j][4][2], results[r]["early"][j][4][3]
+            hinfo = results[r]["early"][j][2]
+            assert (dinfo["first_fail"], dinfo["rounds"], dinfo["searched"]) == \
+                (hinfo["first_fail"], hinfo["rounds"], hinfo["searched"]), (config, r)
+            assert dtot == qdist.totals_from_status(dev_st, dev_nd).tolist()

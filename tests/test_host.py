@@ -36,7 +36,7 @@ def test_abi_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(device.EXPORTS) == set(names)
-    assert device.load_library().qsmd_abi_version() == 2
+    assert device.load_library().qsmd_abi_version() == 3
 
 
 def test_fast_host_entry_forwards_to_the_c_abi():

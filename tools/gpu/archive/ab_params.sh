@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of bench.py settings on one box, alternated (diagnostic):
-#   tools/gpu/ab_params.sh ROUNDS "TAG|ENV|ARGS" ...
+#   tools/gpu/archive/ab_params.sh ROUNDS "TAG|ENV|ARGS" ...
 # ENV: space-separated VAR=VALUE (e.g. QSMD_LIB_PATH=ablib/x.so), may be empty.
 # Each run: bench.py --no-cpu-baseline --no-extra ARGS; prints TAG value stage0/call means.
 R=$1; shift

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Stage-0 time of diagnostic builds (tools/build_variant.sh) and settings:
 # per-launch device times from tools/stage_times.py, one process per case.
-#   tools/gpu/diag_stage0.sh "lib.so [param=value ...]" ...
+#   tools/gpu/archive/diag_stage0.sh "lib.so [param=value ...]" ...
 set -o pipefail
 mkdir -p gpurun_out/diag
 i=0

@@ -4,7 +4,7 @@
 # all-reduce; then a kernel + HIP trace of one rank each way.
 set -o pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-bash tools/gpu/rccl_sweep.sh 3 "none||" "dist|QSMD_BENCH_DIST=1|" "dist_q8|QSMD_BENCH_DIST=1|--hw-queues 8" \
+bash tools/gpu/archive/rccl_sweep.sh 3 "none||" "dist|QSMD_BENCH_DIST=1|" "dist_q8|QSMD_BENCH_DIST=1|--hw-queues 8" \
     "dist_i2|QSMD_BENCH_DIST=1|--inflight 2" "dist_noar|QSMD_BENCH_DIST=1 QSMD_BENCH_NOAR=1|" "none_i2||--inflight 2" \
     > gpurun_out/rccl/sweep.log 2>&1 || { cat gpurun_out/rccl/sweep.log; exit 1; }
 cat gpurun_out/rccl/sweep.log

@@ -2,7 +2,7 @@
 # One-rank cost of the RCCL path (verdict r01 item 6) and the hardware-queue
 # count: bench.py runs with and without RCCL initialised (QSMD_BENCH_DIST=1),
 # with and without the all-reduce (QSMD_BENCH_NOAR=1), per in-flight depth
-# and GPU_MAX_HW_QUEUES.  tools/gpu/rccl_sweep.sh [rounds] "TAG|ENV|ARGS" ...
+# and GPU_MAX_HW_QUEUES.  tools/gpu/archive/rccl_sweep.sh [rounds] "TAG|ENV|ARGS" ...
 set -o pipefail
 R=${1:-3}; shift
 STEPS=${STEPS:-60}

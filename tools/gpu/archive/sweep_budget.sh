@@ -1,7 +1,7 @@
 #!/bin/bash
 # Stage-0 node budget sweep (config 2) with the heavy stage in wave mode:
 # calls in flight (bench default) and one call at a time.
-#   tools/gpu/sweep_budget.sh "16 20 26" [steps]
+#   tools/gpu/archive/sweep_budget.sh "16 20 26" [steps]
 set -o pipefail
 mkdir -p gpurun_out/sweep
 B=${1:-"16 18 20 22 24 26 32"}
