@@ -104,7 +104,10 @@ class InFlight:
                 c.set_stage0_budget(budget0)
             for k, v in knobs:
                 c.set_param(k, v)
-        self.streams = streams or [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+        # (streams of their own: torch's default stream is handle 0, which the
+        # C ABI reads as "the context's stream" -- the all-reduce's wait on it
+        # would not order the counters it reads after that slot's calls)
+        self.streams = streams or [torch.cuda.Stream(dev) for _ in range(S)]
         self.outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
                      for _ in range(S)]
         # counters: [block parity][step of the block][8]; a row is reused two blocks later
@@ -127,7 +130,7 @@ class InFlight:
         self.last = (0, 0, 0, 0)
 
     def _allreduce(self, par):
-        for st_ in self.streams[:-1]:
+        for st_ in self.streams:               # after every slot's last call of the block
             self.comm.wait_stream(st_)
         with torch.cuda.stream(self.comm):
             dist.all_reduce(self.tot[par], op=dist.ReduceOp.SUM)
@@ -177,6 +180,7 @@ class InFlight:
             self.step()
         self.drain()
         torch.cuda.synchronize(self.dev)
+        self.done = [None, None]               # (the warm-up's collectives are complete: no waits on them)
         if self.use_dist:
             dist.barrier(group=self.host_group)
         torch.cuda.synchronize(self.dev)
@@ -317,7 +321,7 @@ def early_exit_leg(dev, rank, world, config, n_per_gpu, steps, warmup, chunk, us
     mid = gen.CONFIGS[config]["model_id"]
     ctx = device.Context(dev.index)
     run = lambda: qdist.check_shard_early_exit_device(ctx, mid, d_hdr, d_ev, len(ev), n_total, rank, world,  # noqa
-                                                      chunk=chunk, group=group)
+                                                      chunk=chunk, group=None)
     for _ in range(warmup):
         run()
     torch.cuda.synchronize(dev)
@@ -358,7 +362,7 @@ def early_exit_leg(dev, rank, world, config, n_per_gpu, steps, warmup, chunk, us
     return out
 
 
-def extra_configs(dev, S, knobs):
+def extra_configs(dev, S, knobs, streams):
     """Bounded runs of BASELINE configs 1, 3, 5 (same in-flight step as the
     headline, the library's stage-0 budget) and 4 (one adversarial 8 x 64 TicketDispenser history, memo
     mode), each checked against the oracle on a sample."""
@@ -369,7 +373,9 @@ def extra_configs(dev, S, knobs):
                                    (5, "bank_6x24", 100_000, 20)):
         hdr, ev, d_hdr, d_ev = device_batch(name, 0, n, dev)
         mid = gen.CONFIGS[name]["model_id"]
-        run = InFlight(dev, mid, d_hdr, n, d_ev, len(ev), S, 1, device.QSMD_FLAG_EXHAUSTIVE, False, knobs, -1)
+        # (the headline's slot streams: the same streams on the same hardware queues)
+        run = InFlight(dev, mid, d_hdr, n, d_ev, len(ev), S, 1, device.QSMD_FLAG_EXHAUSTIVE, False, knobs, -1,
+                       streams=streams)
         el = run.timed(steps, 3)
         st, nd, tot, _ = run.results()
         s0, call = run.ctxs[0].timing_read()
@@ -427,7 +433,7 @@ def main():
                     help="per-call HIP timing events inside the timed window (1: device_ms.in_flight; "
                          "instrumentation, ~13 us per synchronous call)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="calls in flight (one context + stream each); 0 = 3")
+                    help="calls in flight (one context + stream each); 0 = 4 (the extra configs: 3)")
     ap.add_argument("--ar-rounds", type=int, default=16,
                     help="rounds of in-flight steps whose counters one RCCL all-reduce carries (N > 1)")
     ap.add_argument("--device-gen", action="store_true",
@@ -438,14 +444,17 @@ def main():
                     help="time BASELINE config 3's early-termination path instead (bank_4x16_bugs by default, "
                          "1.25M histories per GPU: 10M over 8 GPUs), sharded, QSMD_FLAG_EARLY_EXIT_BATCH")
     ap.add_argument("--chunk", type=int, default=262144, help="--early-exit: histories per rank per round")
-    ap.add_argument("--rotate", type=int, default=1,
-                    help="distinct resident batches of n-hist histories; step s checks batch s %% K (the library's "
-                         "cross-call hints then come from other batches)")
+    ap.add_argument("--rotate", type=int, default=5,
+                    help="distinct resident batches of n-hist histories; step s checks batch s %% K, so the "
+                         "library's cross-call hints come from other batches, as in a stream of new batches "
+                         "(default 5; 1 = every step re-checks one batch)")
+    ap.add_argument("--rotate-copies", action="store_true",
+                    help="diagnostic: --rotate's batches are copies of batch 0 (same hints, no cache reuse)")
     ap.add_argument("--roof-calls", type=int, default=30,
                     help="synchronous calls after the timed region that time the dominant kernel alone")
     args = ap.parse_args()
     args.rotate = max(1, args.rotate)
-    if args.rotate > 1 and args.rotate % (args.inflight or 3) == 0:
+    if args.rotate > 1 and args.rotate % (args.inflight or 4) == 0:
         ap.error("--rotate K must not be a multiple of the calls in flight (each context would see one batch)")
 
     # stdout carries exactly one JSON line (rank 0): RCCL prints a version
@@ -466,10 +475,17 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     use_dist = world > 1 or os.environ.get("QSMD_BENCH_DIST") == "1"
-    S = args.inflight if args.inflight > 0 else 3
+    # 4 calls in flight on the box's 4 hardware queues: one stream's chain
+    # (stage 0, then its heavy stage beside the other streams' stage 0s) is
+    # the pipeline's critical path, and a fourth stream overlaps it -- config
+    # 2 at the driver's 20 steps 8.47-8.91e9 against 7.88-8.50e9 with 3 (5
+    # alternating rounds), 5 or 6 in flight share hardware queues and lose
+    # (7.1-7.5 / 6.7e9; tools/gpu/r05_if.sh, r05_if2.sh).  The extra configs
+    # run at 3: config 1 (2 x 10 TicketDispenser) drops from 9.9 to 6.7e9 at 4
+    S = args.inflight if args.inflight > 0 else 4
     # the slot streams, created and used before RCCL creates its own, so that
     # each gets a hardware queue of its own (GPU_MAX_HW_QUEUES)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]
     comm = torch.cuda.Stream(dev) if use_dist else None
     for st_ in streams + ([comm] if comm is not None else []):
         with torch.cuda.stream(st_):
@@ -543,7 +559,10 @@ def main():
     host_batches = [(hdr, ev)]
     dev_batches = [(d_hdr, d_ev, len(ev))]
     for k in range(1, args.rotate):
-        h_k, e_k, dh_k, de_k = device_batch(args.config, (rank * args.rotate + k) * n, n, dev)
+        if args.rotate_copies:               # diagnostic: the same histories at another address
+            h_k, e_k, dh_k, de_k = hdr, ev, d_hdr.clone(), d_ev.clone()
+        else:
+            h_k, e_k, dh_k, de_k = device_batch(args.config, (rank * args.rotate + k) * n, n, dev)
         host_batches.append((h_k, e_k))
         dev_batches.append((dh_k, de_k, len(e_k)))
     log(f"[rank {rank}] generated {args.rotate} x {n} histories ({'device' if args.device_gen else 'host'}) "
@@ -684,7 +703,8 @@ def main():
         out["checked_vs_oracle"] = len(hdr_l)
         out["checked_batch"] = last_batch
     if rank == 0 and world == 1 and not args.no_extra:
-        out["extra"] = {"configs": extra_configs(dev, S, knobs)}
+        s_x = min(S, 3) if args.inflight <= 0 else S
+        out["extra"] = {"configs": extra_configs(dev, s_x, knobs, streams[:s_x])}
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)
     if use_dist:

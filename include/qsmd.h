@@ -252,6 +252,10 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *   "memo_after"        lane mode: the memo joins a search after this many
  *                       nodes (default 32; before, the plain DFS without the
  *                       probe per node)
+ *   "resume_cap"        lane mode: stage 0's saved search states, slots per
+ *                       heavy-list shard (0 = automatic: twice the last
+ *                       call's heavy count per shard, at least 1024); a heavy
+ *                       history past them starts again at the root
  *   "fold"              lane mode: 1 (default) no stage-0w launch after a
  *                       call that deferred nothing to it (the heavy stage
  *                       takes what stage 0 defers on to the giant stage);
@@ -275,7 +279,7 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
 int qsmd_set_param(qsmd_ctx* ctx, const char* name, uint64_t value);
 
 /* Read a knob ("stage0_budget": 0 while automatic, "fold", "heavy_mode",
- * "memo_after") or "stage0_budget_last": the stage-0 budget the most recent
+ * "memo_after", "resume_cap") or "stage0_budget_last": the stage-0 budget the most recent
  * finished check call ran with (the automatic one included; waits for the
  * context's last call). */
 int qsmd_get_param(qsmd_ctx* ctx, const char* name, uint64_t* out);

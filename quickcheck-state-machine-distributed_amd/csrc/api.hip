@@ -119,6 +119,14 @@ struct qsmd_ctx {
     uint64_t memo_grid = 0;            // heavy stage (lane mode): workgroups at most (0 = 12 per CU); one table each
     uint64_t mt_entries = 128;
     uint64_t memo_after = 32;          // lane mode: the memo joins a search after this many nodes
+    // lane mode: stage 0's saved search states (80 B each), slots per heavy-
+    // list shard: from the last call's heavy count (2x, at least 1024; an
+    // eighth of the batch before the first call), or the knob resume_cap.  A
+    // heavy history past its shard's slots starts again at the root, and a
+    // buffer that cannot be had means no resume at all (the same results)
+    char* rs = nullptr;
+    size_t rs_bytes = 0;
+    uint64_t resume_cap = 0;
     uint32_t memo_lds_entries = 64;             // LDS tables: entries per lane (power of two, 4..64)
     uint64_t memo_lds_cap = 0;                  // diagnostic: LDS-table bytes accepted at most (0 = the device's)
     char* mt = nullptr;
@@ -162,6 +170,18 @@ int fail(qsmd_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
         c->err = buf;
     }
     return code;
+}
+
+// The context's own stream (host entry points, device calls given no
+// stream), created on first use: a caller that always passes its streams
+// (bench.py's calls in flight) leaves no idle stream sharing the device's
+// hardware queues with the ones it uses.
+hipStream_t ctx_stream(qsmd_ctx* c) {
+    if (!c->stream && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        c->stream = nullptr;
+    }
+    return c->stream;
 }
 
 // QSMD_SYNC_STAGES=1 (diagnostic): synchronise after every launch of the
@@ -301,8 +321,7 @@ int qsmd_open(qsmd_ctx** out, int device) {
     if (device < 0 || device >= n) return QSMD_ERR_ARG;
     auto* c = new qsmd_ctx();
     c->device = device;
-    if (hipSetDevice(device) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess) {
         delete c;
         return QSMD_ERR_DEVICE;
     }
@@ -332,6 +351,7 @@ void qsmd_close(qsmd_ctx* c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->sx) (void)hipFree(c->sx);
     if (c->mt) (void)hipFree(c->mt);
+    if (c->rs) (void)hipFree(c->rs);
     if (c->xm) (void)hipFree(c->xm);
     if (c->memo) (void)hipFree(c->memo);
     if (c->io) (void)hipFree(c->io);
@@ -428,6 +448,8 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "memo_lds") {
         if (value > 2) return fail(c, QSMD_ERR_ARG, "memo_lds: 0 = HBM tables, 1 = LDS for short lists, 2 = LDS");
         c->memo_lds = (uint32_t)value;
+    } else if (n == "resume_cap") {          // lane mode: saved-state slots per heavy-list shard (0 = auto)
+        c->resume_cap = value;
     } else if (n == "fold") {
         if (value > (QSMD_DIAG_FOLD2 ? 2u : 1u))
             return fail(c, QSMD_ERR_ARG, "fold: 0 or 1 (no stage-0w launch; 2, no giant launch either: diagnostic builds)");
@@ -528,7 +550,13 @@ static bool lane_tables(qsmd_ctx* c, hipStream_t s, uint64_t grid) {
     const size_t need = (size_t)grid * 64 * c->mt_entries * (32 + 64);
     if (c->mt_bytes >= need) return true;
     bool re = false;
-    if (grow(c, &c->mt, &c->mt_bytes, need, &re) != QSMD_OK) {
+    // (with headroom: the grid follows the last call's heavy count, and a
+    // stream of distinct batches moves it a little every call -- sized to
+    // the count alone, the tables grew, were cleared and waited for the
+    // context's last call in the middle of a caller's stream of calls:
+    // 4.8 vs 8.8e9 histories/s over five resident batches, tools/gpu/r05_rot2.sh)
+    if (grow(c, &c->mt, &c->mt_bytes, need + need / 2, &re) != QSMD_OK &&
+        grow(c, &c->mt, &c->mt_bytes, need, &re) != QSMD_OK) {
         (void)hipGetLastError();
         return false;
     }
@@ -651,8 +679,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const size_t off_tn = off_ts + align_up(n_tk);
     const size_t off_tw = off_tn + align_up(n_tk * 8);
     const size_t off_nd = off_tw + (want_w ? align_up(n_tk * kTaskWitness) : 0);   // nodes if the caller has none
-    const size_t off_rs = off_nd + (early && !nodes ? align_up(n_hist * 8) : 0);   // stage 0's saved states
-    const size_t off_tot = off_rs + (lane ? align_up(kShards * cap32 * kResumeWords * 4) : 0);
+    const size_t off_tot = off_nd + (early && !nodes ? align_up(n_hist * 8) : 0);
     const size_t need = off_tot + align_up(sizeof(qsmd_totals));
     bool re = false;
     rc = grow(c, &c->ws, &c->ws_bytes, need, &re);
@@ -666,7 +693,22 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     uint32_t* l0 = reinterpret_cast<uint32_t*>(c->ws + off_l0);
     uint32_t* h32 = reinterpret_cast<uint32_t*>(c->ws + off_h32);
     uint32_t* shards = reinterpret_cast<uint32_t*>(c->ws + kOffShards);
-    uint32_t* states = lane ? reinterpret_cast<uint32_t*>(c->ws + off_rs) : nullptr;
+    // stage 0's saved states (lane mode): their own buffer, slots per shard capped
+    uint64_t rs_cap = 0;
+    uint32_t* states = nullptr;
+    if (lane) {
+        rs_cap = c->resume_cap ? c->resume_cap
+                               : (c->probe_valid ? std::max<uint64_t>(1024, 2ull * hint[1] / kShards) : cap32 / 8);
+        rs_cap = std::min<uint64_t>(std::max<uint64_t>(rs_cap, 1), cap32);
+        const size_t rs_need = (size_t)kShards * rs_cap * kResumeWords * 4;
+        if (c->rs_bytes >= rs_need || grow(c, &c->rs, &c->rs_bytes, rs_need + rs_need / 2) == QSMD_OK ||
+            grow(c, &c->rs, &c->rs_bytes, rs_need) == QSMD_OK) {   // (headroom: see lane_tables)
+            states = reinterpret_cast<uint32_t*>(c->rs);
+        } else {
+            (void)hipGetLastError();
+            c->err.clear();
+        }
+    }
     uint32_t* h64 = reinterpret_cast<uint32_t*>(c->ws + off_h64);
     uint32_t* lw = reinterpret_cast<uint32_t*>(c->ws + off_lw);
     uint32_t* lg = reinterpret_cast<uint32_t*>(c->ws + off_lg);
@@ -746,7 +788,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.heavy_count = shards;
     a0.heavy_shard_cap = (uint32_t)cap32;
     a0.heavy_state = states;                 // (lane mode goes on from them)
-    a0.stage0_budget = budget0 ? budget0 : ~0ull;
+    a0.heavy_state_cap = (uint32_t)rs_cap;
+    // (below 2^31: a saved state keeps its node count in 32 bits)
+    a0.stage0_budget = budget0 ? std::min<uint64_t>(budget0, 0x7FFFFFFFull) : ~0ull;
     a0.stamps = c->s0_stamps;
     const uint64_t n_groups = std::max<uint64_t>((n_hist + 63) / 64, 1);
     stage_done("start", s, cnt);
@@ -794,6 +838,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].entries = (uint32_t)c->mt_entries;
             mp[w].memo_after = (uint32_t)std::min<uint64_t>(c->memo_after, 0xFFFFFFFFull);
             mp[w].resume = w ? nullptr : states;
+            mp[w].resume_cap = (uint32_t)rs_cap;
             mp[w].lds_entries = lds_entries;
             mp[w].epoch = c->mt_epoch;
             mp[w].giant_cap = cap;
@@ -867,7 +912,8 @@ int qsmd_check_batch_device(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr_
                             uint8_t* witness_dev, qsmd_totals* totals_dev, void* stream) {
     if (!c) return QSMD_ERR_ARG;
     std::lock_guard<std::mutex> g(c->mu);
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx_stream(c);
+    if (!s) return fail(c, QSMD_ERR_DEVICE, "hipStreamCreate");
     return check_device_locked(c, model_id, hdr_dev, n_hist, events_dev, n_events, model0_host, flags,
                                max_nodes, status_dev, nodes_dev, witness_dev, totals_dev, s);
 }
@@ -899,7 +945,8 @@ int qsmd_check_batch(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, uint64
     if (n_events && !events) return fail(c, QSMD_ERR_ARG, "null events");
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
-    hipStream_t s = c->stream;
+    hipStream_t s = ctx_stream(c);
+    if (!s) return fail(c, QSMD_ERR_DEVICE, "hipStreamCreate");
     HIP_TRY(c, order_after_previous(c, s), "order after the previous call");
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness_out;
     // io layout: [hdr | events | witness] copied in, [witness | status | nodes | totals] copied out
@@ -1013,7 +1060,7 @@ int qsmd_gen_batch_device(qsmd_ctx* c, const qsmd_gen_params* p, uint64_t first,
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     HIP_TRY(c, launch_gen(*p, first, n_hist, ev_base, hdr_dev, events_dev, bug_dev,
-                          stream ? static_cast<hipStream_t>(stream) : c->stream), "gen launch");
+                          stream ? static_cast<hipStream_t>(stream) : ctx_stream(c)), "gen launch");
     return QSMD_OK;
 }
 
@@ -1024,7 +1071,7 @@ int qsmd_wellformed_batch_device(qsmd_ctx* c, const qsmd_hdr* hdr_dev, uint64_t 
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
     return wellformed_locked(c, hdr_dev, n_hist, events_dev, n_events, pids, n_pids, out_dev,
-                             stream ? static_cast<hipStream_t>(stream) : c->stream);
+                             stream ? static_cast<hipStream_t>(stream) : ctx_stream(c));
 }
 
 int qsmd_wellformed_batch(qsmd_ctx* c, const qsmd_hdr* hdr, uint64_t n_hist, const qsmd_event* events,
@@ -1034,7 +1081,8 @@ int qsmd_wellformed_batch(qsmd_ctx* c, const qsmd_hdr* hdr, uint64_t n_hist, con
     if (n_events && !events) return fail(c, QSMD_ERR_ARG, "null events");
     std::lock_guard<std::mutex> g(c->mu);
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
-    hipStream_t s = c->stream;
+    hipStream_t s = ctx_stream(c);
+    if (!s) return fail(c, QSMD_ERR_DEVICE, "hipStreamCreate");
     const size_t o_ev = align_up(n_hist * sizeof(qsmd_hdr));
     const size_t o_out = o_ev + align_up(n_events * sizeof(qsmd_event));
     int rc = grow(c, &c->io, &c->io_bytes, o_out + align_up(n_hist * sizeof(qsmd_wf)));
@@ -1108,6 +1156,8 @@ int qsmd_get_param(qsmd_ctx* c, const char* name, uint64_t* out) {
         *out = c->probe_host[kProbeBudget];
     } else if (n == "stage0_budget") {       // the set budget, 0 while automatic
         *out = c->s0_auto ? 0 : c->stage0_budget;
+    } else if (n == "resume_cap") {
+        *out = c->resume_cap;
     } else if (n == "fold") {
         *out = c->fold;
     } else if (n == "heavy_mode") {
@@ -1163,7 +1213,8 @@ int qsmd_split_frontier(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, con
         return QSMD_OK;
     }
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
-    hipStream_t s = c->stream;
+    hipStream_t s = ctx_stream(c);
+    if (!s) return fail(c, QSMD_ERR_DEVICE, "hipStreamCreate");
     quiesce(c);
     const uint64_t cap = std::max<uint64_t>(max_tasks, 1);
     const uint32_t v = split_variant(hdr);
@@ -1242,7 +1293,8 @@ int qsmd_check_tasks(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, const 
     if (rc) return rc;
     if (!n_tasks) return QSMD_OK;
     HIP_TRY(c, hipSetDevice(c->device), "hipSetDevice");
-    hipStream_t s = c->stream;
+    hipStream_t s = ctx_stream(c);
+    if (!s) return fail(c, QSMD_ERR_DEVICE, "hipStreamCreate");
     quiesce(c);
     const uint32_t v = split_variant(hdr);
     const uint64_t n = n_tasks;

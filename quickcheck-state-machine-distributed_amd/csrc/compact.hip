@@ -225,8 +225,8 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
             const uint32_t at = wave_append(heavy, h, a.heavy_list + (uint64_t)k * a.heavy_shard_cap,
                                             a.heavy_count + k * kShardStride, lane);
             if constexpr (G::EV == 32) {
-                if (heavy && a.heavy_state)
-                    dfs.save(a.heavy_state + ((uint64_t)k * a.heavy_shard_cap + at) * kResumeWords, s_bal, lane);
+                if (heavy && a.heavy_state && at < a.heavy_state_cap)
+                    dfs.save(a.heavy_state + ((uint64_t)k * a.heavy_state_cap + at) * kResumeWords, s_bal, lane);
             }
         } else {
             wave_append(heavy, h, a.heavy_list, a.heavy_count, lane);

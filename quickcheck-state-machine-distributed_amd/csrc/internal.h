@@ -132,8 +132,11 @@ struct SearchArgs {
     uint32_t* heavy_list;
     uint32_t* heavy_count;
     uint32_t heavy_shard_cap;     // > 0: heavy_list / heavy_count sharded (kShards)
-    uint32_t* heavy_state;        // stage 0: a heavy history's search state at the budget, at its list
-                                  // position (kResumeWords words; null = the heavy stage starts at the root)
+    uint32_t* heavy_state;        // stage 0: a heavy history's search state at the budget, slot k x
+                                  // heavy_state_cap + (its position in shard k), kResumeWords words each;
+                                  // positions past heavy_state_cap save nothing (the heavy stage starts
+                                  // those at the root); null = no saved states
+    uint32_t heavy_state_cap;
     uint64_t stage0_budget;
     uint32_t flags;
     uint32_t model_id;
@@ -307,6 +310,7 @@ struct MemoArgs {
     uint32_t entries;
     uint32_t memo_after;          // no memo probe / insert before a search has counted this many nodes
     const uint32_t* resume;       // G32 list: stage 0's saved states (SearchArgs::heavy_state), or null
+    uint32_t resume_cap;          // their slots per shard (SearchArgs::heavy_state_cap)
     uint32_t lds_entries;         // LDS tables (lds_tables): entries per lane, a power of two <= 64
     uint32_t epoch;               // this call's tag (24 bits)
     uint64_t giant_cap;           // > 0: a search past this many iterations goes to s.giant_list

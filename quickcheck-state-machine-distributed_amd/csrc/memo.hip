@@ -39,6 +39,9 @@
 #ifndef QSMD_DIAG_FOLD2
 #define QSMD_DIAG_FOLD2 0
 #endif
+#ifndef QSMD_DIAG_MEMOPRIO
+#define QSMD_DIAG_MEMOPRIO 0
+#endif
 
 namespace qsmd {
 
@@ -296,8 +299,12 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
             // go on from stage 0's state at its budget (the nodes it counted
             // stay counted); the levels entered there have no entry count,
             // so they are never recorded in the memo when they fail
-            if (p.resume) {
-                dfs.restore(p.resume + pos * kResumeWords, L.bal, lane);
+            // (the saved state's slot: shard k = pos / cap, its position in the
+            // shard pos % cap; none past resume_cap)
+            const uint32_t cap = a.list_shard_cap;
+            const uint64_t within = cap ? pos % cap : pos;
+            if (p.resume && within < p.resume_cap) {
+                dfs.restore(p.resume + ((cap ? pos / cap : 0u) * p.resume_cap + within) * kResumeWords, L.bal, lane);
                 for (uint32_t d = 0; d < dfs.depth; ++d) L.entry[d][lane] = kNoEntry;
             }
         }
@@ -366,6 +373,9 @@ template <uint32_t MODEL, bool LT>
 __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(SplitArgs t, MemoArgs p32, MemoArgs p64,
                                                                    uint32_t wide, uint32_t fold) {
     extern __shared__ uint32_t lds[];
+#if QSMD_DIAG_MEMOPRIO
+    __builtin_amdgcn_s_setprio(QSMD_DIAG_MEMOPRIO);   // diagnostic builds: issue priority over stage 0's waves
+#endif
     const int lane = threadIdx.x;
     const uint64_t n32 = (list_total(p32.s.list_count, p32.s.list_shard_cap) + 63u) / 64u,
                    n64 = (list_total(p64.s.list_count, p64.s.list_shard_cap) + 63u) / 64u;

@@ -185,8 +185,8 @@ def check_shard_early_exit_device(ctx, model_id, d_hdr, d_ev, n_events, n_total,
     skipped count -- and one MIN all-reduce per round (RCCL on a device
     tensor under nccl) publishes the global first failure; its 8-byte result
     is the only value that reaches the host per round, for the decision to
-    stop.  Status and node arrays stay on the device.  Everything runs on the
-    current torch stream.  Same rounds, stopping
+    stop.  Status and node arrays stay on the device.  The calls and the torch
+    ops run on a stream of their own, ordered after the caller's.  Same rounds, stopping
     rule and final SKIPPED marking as the host version, so status, nodes and
     totals equal one context's early exit over the concatenated batch.
 
@@ -210,7 +210,27 @@ def check_shard_early_exit_device(ctx, model_id, d_hdr, d_ev, n_events, n_total,
     searched = torch.zeros((), dtype=torch.int64, device=dev)
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
     cdev = _collective_device(group) if multi else dev
-    s = torch.cuda.current_stream(dev).cuda_stream          # the calls and the torch ops below: one stream
+    # the calls and the torch ops below on one stream of their own (torch's
+    # default stream is handle 0, which the C ABI reads as "the context's
+    # stream": nothing would order the two), joined to the caller's at the end
+    caller = torch.cuda.current_stream(dev)
+    st_ = torch.cuda.Stream(dev)
+    st_.wait_stream(caller)
+    with torch.cuda.stream(st_):
+        out = _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, rounds_all, chunk,
+                            status, nodes, tot, local, searched, multi, cdev, group, max_nodes, st_.cuda_stream)
+    caller.wait_stream(st_)
+    return out
+
+
+def _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, rounds_all, chunk, status,
+                  nodes, tot, local, searched, multi, cdev, group, max_nodes, s):
+    import torch
+    import torch.distributed as dist
+
+    from . import device
+
+    dev = d_hdr.device
     flags = device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_EARLY_EXIT_BATCH
     best, rounds = n_total, 0
     for k in range(rounds_all):

@@ -139,7 +139,7 @@ def test_random_any_shape(ctx, model):
 
 DEFAULTS = {"stage0_budget": 32, "memo_after": 32, "stage0_grid": 65536, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
             "wave_grid": 0, "split_budget": 1024, "memo_lane_entries": 128, "memo_grid": 0, "split_xmemo": 1,
-            "memo_lds": 1, "memo_lds_entries": 64, "dag_states": 128, "memo_lds_cap": 0}
+            "memo_lds": 1, "memo_lds_entries": 64, "dag_states": 128, "memo_lds_cap": 0, "fold": 1, "resume_cap": 0}
 
 
 @pytest.fixture
@@ -680,17 +680,18 @@ def test_bench_knobs_in_flight_full_size(name, n):
 
 @pytest.mark.parametrize("packed", [True, False])
 def test_value_ranges_and_pairing(ctx, packed):
-    """Stage 0 holds invocation values within 14-bit signed and response
-    values within 25-bit signed; anything wider goes to stage 1.  Put values
-    on both sides of both bounds into generated Bank histories (packed
-    uniform batch and a non-uniform one), and mix paired (every pid
-    alternates) with unpaired histories inside one wavefront."""
+    """Stage 0 holds invocation values within 9-bit signed (-256..255) and
+    response values within 25-bit signed (lane.h IVAL_BITS / RVAL_BITS);
+    anything wider goes on to the next stage.  Put values on both sides of
+    both bounds into generated Bank histories (packed uniform batch and a
+    non-uniform one), and mix paired (every pid alternates) with unpaired
+    histories inside one wavefront."""
     hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 7, 64 * 40)
     ev = ev.copy()
     nr = np.random.default_rng(11)
     inv = np.nonzero((ev["kp"] & 0x80) == 0)[0]
     rsp = np.nonzero(((ev["kp"] & 0x80) != 0) & (ev["code"] == 7))[0]        # Balance responses
-    iv = np.array([8191, 8192, -8192, -8193, 1 << 20, -(1 << 30)], dtype=np.int32)
+    iv = np.array([255, 256, -256, -257, 8191, 8192, -8192, -8193, 1 << 20, -(1 << 30)], dtype=np.int32)
     rv = np.array([(1 << 24) - 1, 1 << 24, -(1 << 24), -(1 << 24) - 1, 1 << 30], dtype=np.int32)
     ki = nr.choice(inv, 300, replace=False)
     kr = nr.choice(rsp, 300, replace=False)
@@ -705,3 +706,92 @@ def test_value_ranges_and_pairing(ctx, packed):
     if not packed:
         hdr = hdr[nr.permutation(len(hdr))]
     _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**6)
+
+
+def _concat(*batches):
+    """One batch of several (hdr, events) batches, headers rebased."""
+    hs, es, off = [], [], 0
+    for hdr, ev in batches:
+        h = hdr.copy()
+        h["ev_off"] += off
+        hs.append(h)
+        es.append(ev)
+        off += len(ev)
+    return np.concatenate(hs), np.concatenate(es)
+
+
+@pytest.mark.parametrize("fold", [0, 1])
+def test_fold_stage0w(ctx, knobs, fold):
+    """Lane mode's folded tail (knob fold 1, the default): after a call that
+    deferred nothing to stage 0w, the next launches no stage 0w -- what stage
+    0 defers then goes on to the giant stage.  A call stream whose deferred
+    count changes under it (clean 4x16 batches, then a batch mixing in 6x24
+    histories and wider ones, then clean again) stays the oracle's, and the
+    probe still counts what stage 0 deferred."""
+    knobs(heavy_mode=1, memo_lds=0, stage0_budget=16, fold=fold)
+    b2 = gen.generate_config("bank_4x16", 21, 20000)[:2]
+    b5 = gen.generate_config("bank_6x24", 21, 3000)[:2]
+    rng = random.Random(8)
+    wide = codec.encode(models.BANK, [histgen.wellformed_history(rng, "bank", rng.randint(33, 60), rng.randint(2, 8),
+                                                                 p_pending=0.0) for _ in range(200)])
+    mixed = _concat(b2, b5, (wide.hdr, wide.events))
+    for hdr, ev in (b2, b2, mixed, b2, mixed, mixed, b2):
+        _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**7)
+        assert ctx.probe()["deferred"] == (3200 if len(hdr) > 20000 else 0)
+
+
+@pytest.mark.parametrize("cap", [1, 7, 64])
+def test_resume_cap(ctx, knobs, cap):
+    """Lane mode's saved stage-0 states are capped per heavy-list shard
+    (knob resume_cap; by default from the last call's heavy count): a heavy
+    history past its shard's slots starts again at the root.  Exact either
+    way, on the bug-laden batch with many heavy histories and a clean one."""
+    knobs(heavy_mode=1, memo_lds=0, stage0_budget=8, resume_cap=cap)
+    for name in ("bank_4x16_bugs", "bank_4x16"):
+        hdr, ev, _ = gen.generate_config(name, 5, 20000)
+        _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**7)
+
+
+def test_host_waits_stay_with_the_context():
+    """A context's host waits (qsmd_probe_read here) wait for that context's
+    last call only -- its completion event or its one stream -- not for the
+    device: context A's giant stage (one workgroup) is held back half a
+    second (the giant_stall_us diagnostic) on stream sA while context B, on stream sB,
+    finishes a call and reads its probe; sA is still busy when that returns.
+    Both calls' results are the oracle's."""
+    torch = pytest.importorskip("torch")
+    import time
+    dev = torch.device("cuda:0")
+    rng = random.Random(31)
+    ga = codec.encode(models.BANK, [histgen.wellformed_history(rng, "bank", 30, 12, p_pending=0.0)
+                                    for _ in range(8)])                    # > 8 pids: the giant stage
+    hb, eb, _ = gen.generate_config("bank_4x16", 3, 5000)
+    A, B = device.Context(0), device.Context(0)
+    sA, sB = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    try:
+        A.set_param("giant_stall_us", 500000)
+        A.set_param("giant_grid", 1)              # (A's stalled giant stage holds one CU, not the GPU)
+        bufs = []
+        for hdr, ev in ((ga.hdr, ga.events), (hb, eb)):
+            n = len(hdr)
+            bufs.append((torch.from_numpy(hdr.view(np.uint8)).to(dev), torch.from_numpy(ev.view(np.uint8)).to(dev),
+                         torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev)))
+        torch.cuda.synchronize()
+        (ha, ea, sta, nda), (hbd, ebd, stb, ndb) = bufs
+        A.check_device(models.MODEL_BANK, ha.data_ptr(), len(ga.hdr), ea.data_ptr(), len(ga.events), sta.data_ptr(),
+                       nda.data_ptr(), None, None, max_nodes=10**6, stream=sA.cuda_stream)
+        t0 = time.perf_counter()
+        B.check_device(models.MODEL_BANK, hbd.data_ptr(), len(hb), ebd.data_ptr(), len(eb), stb.data_ptr(),
+                       ndb.data_ptr(), None, None, max_nodes=10**6, stream=sB.cuda_stream)
+        B.probe()                                   # waits for B's call only
+        waited = time.perf_counter() - t0
+        busy = not sA.query()
+        torch.cuda.synchronize()
+        assert busy and waited < 0.4, (busy, waited)
+        for (hdr, ev), st, nd in (((ga.hdr, ga.events), sta, nda), ((hb, eb), stb, ndb)):
+            st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr, ev, None, 10**6, 8)
+            assert np.array_equal(st.cpu().numpy(), st_o)
+            assert np.array_equal(nd.cpu().numpy().astype(np.uint64), nd_o.astype(np.uint64))
+    finally:
+        A.close()
+        B.close()
