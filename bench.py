@@ -454,7 +454,7 @@ def main():
                     help="synchronous calls after the timed region that time the dominant kernel alone")
     args = ap.parse_args()
     args.rotate = max(1, args.rotate)
-    if args.rotate > 1 and args.rotate % (args.inflight or 4) == 0:
+    if args.rotate > 1 and (args.inflight or 4) > 1 and args.rotate % (args.inflight or 4) == 0:
         ap.error("--rotate K must not be a multiple of the calls in flight (each context would see one batch)")
 
     # stdout carries exactly one JSON line (rank 0): RCCL prints a version
@@ -573,7 +573,7 @@ def main():
     # and lane mode's memo joins after 32 nodes (round 4), 17-20 measure
     # within the spread on config 2 at this command (7.90-8.30e9 at 18; 7.6-7.7
     # at 16; 7.59 at 26 before; tools/gpu/archive/r04_knobs2.sh)
-    budget0 = args.stage0_budget if args.stage0_budget is not None else (18 if S > 1 else -1)
+    budget0 = args.stage0_budget if args.stage0_budget is not None else (20 if S > 1 else -1)
     knobs = [(kv.split("=")[0], int(kv.split("=")[1])) for kv in args.param]
     # with calls in flight the heavy stage runs in lane mode (64 searches per
     # wavefront: a few dozen wavefronts beside the next call's stage 0) with

@@ -23,9 +23,6 @@
 #include "internal.h"
 #include "qsmd_gen.h"
 
-#ifndef QSMD_DIAG_FOLD2
-#define QSMD_DIAG_FOLD2 0
-#endif
 #include "qsmd.h"
 
 using namespace qsmd;
@@ -105,13 +102,12 @@ struct qsmd_ctx {
     // 0 / 1 forces wave / lane mode, 2 (default) picks
     uint64_t heavy_mode = 2;
     uint64_t wave_max = 16384;
-    // lane mode's folded tail (memo.hip): a call whose predecessor deferred
-    // nothing to stage 0w and had no giants launches stage 0 and the heavy
-    // stage only -- the heavy stage's last workgroup finishes the call.  With
-    // calls in flight each launch of a call's chain waits for dispatch behind
-    // the other streams' stage 0 (round 4's trace: the empty stage 0w 25 us and
-    // the giant stage's short path 17 us per call on average, 4 us alone).
-    // 0 = never; the library stops folding once a folded call meets giants
+    // lane mode's folded tail: a call whose predecessor deferred nothing to
+    // stage 0w launches no stage 0w (what stage 0 defers goes on to the giant
+    // stage through the heavy stage); 0 = every call launches it.  With calls
+    // in flight each launch of a call's chain waits for dispatch behind the
+    // other streams' stage 0 (round 4's trace: the empty stage 0w 25 us a call
+    // on average, 4 us alone)
     uint64_t fold = 1;
     uint32_t* probe_host = nullptr;    // pinned: [defer, heavy32, heavy64, giant, timed] of the last finished call
     uint32_t* debug_host = nullptr;    // QSMD_SYNC_STAGES: giant-stage heartbeat (pinned)
@@ -451,8 +447,7 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "resume_cap") {          // lane mode: saved-state slots per heavy-list shard (0 = auto)
         c->resume_cap = value;
     } else if (n == "fold") {
-        if (value > (QSMD_DIAG_FOLD2 ? 2u : 1u))
-            return fail(c, QSMD_ERR_ARG, "fold: 0 or 1 (no stage-0w launch; 2, no giant launch either: diagnostic builds)");
+        if (value > 1) return fail(c, QSMD_ERR_ARG, "fold: 0 or 1");
         c->fold = value;
     } else if (n == "heavy_mode") {
         if (value > 2) return fail(c, QSMD_ERR_ARG, "heavy_mode: 0 = wave, 1 = lane, 2 = auto");
@@ -623,8 +618,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // block sets the probe's written flag)
     if (!c->probe_valid && c->any_call && __atomic_load_n(&c->probe_host[kProbeWritten], __ATOMIC_ACQUIRE))
         c->probe_valid = true;
-    uint32_t hint[10];
-    for (int i = 0; i < 10; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
+    uint32_t hint[9];
+    for (int i = 0; i < 9; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
     const uint64_t budget0 = stage0_budget_of(c, hint);
     // the automatic budget just went down: the last call's heavy count (at
     // the higher budget) undercounts this one's -- size the tail for a long
@@ -654,14 +649,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
                                                       : (uint64_t)c->n_cu);   // (no hint: grid-stride)
     if (lane && !(lt && !wide)) lane = lane_tables(c, s, mg);
     // the folded tail (lane mode, ctx.fold): the last call deferred nothing
-    // to stage 0w and had a normal route -- no stage-0w launch (fold0w); and
-    // with fold 2, when it had no giants either and this call has no early
-    // exit, no giant launch (fold).  A folded call that met giants anyway
-    // (the heavy stage's solo fallback, slow) turns fold 2 off for the context
-    const bool fold0w = lane && c->fold >= 1 && c->probe_valid && route == 0u && !sync_stages() &&
-                        hint[0] == 0u && hint[2] == 0u;
-    const bool fold = fold0w && c->fold >= 2 && !early && hint[3] == 0u && hint[kProbeFold] == 0u;
-    if (c->probe_valid && hint[kProbeFold] != 0u && c->fold >= 2) c->fold = 1;
+    // to stage 0w and this one has a normal route -- no stage-0w launch
+    const bool fold = lane && c->fold && c->probe_valid && route == 0u && !sync_stages() &&
+                      hint[0] == 0u && hint[2] == 0u;
 
     // ---- workspace: header, lists, giant records, tasks
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
@@ -732,8 +722,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a.giant_count = cnt + C_GIANT;
     const bool split = c->split_budget && (!max_nodes || c->split_budget < max_nodes);
 
-    // ---- the giant stage's arguments (its launch, or the folded tail's last
-    // workgroup: the split search, the combine, (the fixup), the totals)
+    // ---- the giant stage's arguments: the split search, the combine, (the
+    // fixup), the totals
     SplitArgs p{};
     p.s = a;
     p.cnt = cnt;
@@ -812,7 +802,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     aw.heavy_list = h64;
     aw.heavy_count = cnt + C_HEAVY64;
     aw.stage0_budget = c->stage0w_budget ? c->stage0w_budget : ~0ull;
-    if (!(route & kSkip0w) && !fold0w)
+    if (!(route & kSkip0w) && !fold)
         HIP_TRY(c, launch_compact64(aw, (uint32_t)((route & kSkip0) ? std::min<uint64_t>(n_groups, kStage0wGrid)
                                                                     : (hint[0] == 0u ? 8u   // (last call: none)
                                                                                      : tail_grid(2ull * c->n_cu, kStage0wGrid,
@@ -831,8 +821,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         for (int w = 0; w < 2; ++w) {
             mp[w].s = a;
             // (folded: no stage 0w ran, G64 groups are stage 0's deferred histories)
-            mp[w].s.list = w ? (fold0w ? l0 : h64) : h32;
-            mp[w].s.list_count = w ? cnt + (fold0w ? C_DEFER : C_HEAVY64) : shards;
+            mp[w].s.list = w ? (fold ? l0 : h64) : h32;
+            mp[w].s.list_count = w ? cnt + (fold ? C_DEFER : C_HEAVY64) : shards;
             mp[w].s.list_shard_cap = w ? 0u : (uint32_t)cap32;
             mp[w].table = reinterpret_cast<uint32_t*>(c->mt + (w ? slots * 32 : 0));
             mp[w].entries = (uint32_t)c->mt_entries;
@@ -847,7 +837,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].fwd_list = lw;                 // stage 0w's deferred histories: on to the giant stage
             mp[w].fwd_count = cnt + C_WIDE;
         }
-        HIP_TRY(c, launch_memo(mp[0], mp[1], (uint32_t)mg, wide, lt, fold, p, s, tm ? evs[3] : nullptr,
+        HIP_TRY(c, launch_memo(mp[0], mp[1], (uint32_t)mg, wide, lt, s, tm ? evs[3] : nullptr,
                                tm ? evs[4] : nullptr), "memo launch");
         stage_done("lane", s, cnt);
     } else {
@@ -885,7 +875,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         HIP_TRY(c, launch_wave(wp, (route & kSkip0w) ? 0u : (uint32_t)g, (uint32_t)g128, s), "wave launch");
         stage_done("wave", s, cnt);
     }
-    if (!fold) {
+    {
         const uint64_t gg = c->giant_grid ? c->giant_grid : (early || hint[3] ? 2ull * c->n_cu : 64ull);
         if (sync_stages()) p.debug = giant_debug_buffer(c, gg);
         HIP_TRY(c, launch_giants(p, (uint32_t)gg, s), "giant launch");

@@ -37,16 +37,6 @@
 #ifndef QSMD_DIAG_STAGE0
 #define QSMD_DIAG_STAGE0 0
 #endif
-// QSMD_DIAG_L2=1: every group stages the inputs of the batch's first 64
-// groups (outputs to its own histories): stage 0 with its HBM reads replaced
-// by L2 hits, to tell the memory system's part from the rest.
-#ifndef QSMD_DIAG_L2
-#define QSMD_DIAG_L2 0
-#endif
-// QSMD_DIAG_SEARCH2=1: every search twice (its marginal cost)
-#ifndef QSMD_DIAG_SEARCH2
-#define QSMD_DIAG_SEARCH2 0
-#endif
 // QSMD_DIAG_NOHEAVY=1: no heavy-list append (the budget-stopped histories
 // are reported BUDGET), to price the append
 #ifndef QSMD_DIAG_NOHEAVY
@@ -109,11 +99,7 @@ __device__ __forceinline__ int stage_fresh(const SearchArgs& a, bool fresh, uint
                                            int32_t (*s_bal)[C_LANES], int lane, LaneDFS<MODEL, G>& dfs,
                                            qsmd_hdr& H) {
     using M = typename G::M;
-#if QSMD_DIAG_L2
-    if (fresh) H = a.hdr[h & 4095u];
-#else
     if (fresh) H = a.hdr[h];
-#endif
     else H = qsmd_hdr{0, 0, 0, 0, 0, 0};
     const uint32_t n_ev = H.n_ev, n_pid = H.n_pid;
     const bool enc_ok = fresh && H.model_id == MODEL && n_ev <= QSMD_MAX_EVENTS && n_pid <= QSMD_MAX_PIDS &&
@@ -197,18 +183,6 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
                                  : lane == 4 ? rt2 : lane == 5 ? (uint64_t)it : rt_entry;
                 a.stamps[g * 8 + lane] = v;
             }
-        }
-#elif QSMD_DIAG_SEARCH2
-        // diagnostic build: every search runs twice (the second from the same
-        // initial state), to price the search's marginal cost
-        if (search) {
-            const LaneDFS<MODEL, G> d0 = dfs;
-            status = run_search(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
-            dfs = d0;
-            if constexpr (MODEL == QSMD_MODEL_BANK)
-                for (int q = 0; q < QSMD_BANK_MAX_ACCOUNTS; ++q)
-                    s_bal[q][lane] = ((a.m0_exists >> q) & 1u) ? (int32_t)a.m0_val[q] : 0;
-            status = run_search(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
         }
 #else
         // the general path (pid masks): finish_lane does not pair (lane.h)

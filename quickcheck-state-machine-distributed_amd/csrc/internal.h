@@ -61,7 +61,6 @@ enum Cnt : uint32_t {
     C_XDONE,            // fixup chunks finished
     C_EXIT,             // giant-stage blocks finished
     C_WIDE,             // stage 0w -> wave mode's wide list (or, in lane mode, on to the giant stage)
-    C_MEXIT,            // folded lane-mode tail: heavy-stage workgroups finished (memo.hip)
     C_N = 32
 };
 
@@ -173,7 +172,6 @@ constexpr int kProbeWide = 5;
 constexpr int kProbeBudget = 6;   // the call's stage-0 budget and batch size (api.hip: the automatic budget)
 constexpr int kProbeN = 7;
 constexpr int kProbeWritten = 8;  // 1 once a call's giant stage wrote the probe (never reset)
-constexpr int kProbeFold = 9;     // 1 once a folded call met giants (memo.hip's solo fallback; never reset)
 
 // internal status: the search was handed to a later stage (not a result)
 constexpr int QSMD_STATUS_HANDED_OFF = 0x40;
@@ -320,12 +318,10 @@ struct MemoArgs {
     const uint32_t* fwd_count;
 };
 // lds_tables: the G32 memo tables in LDS (ignored with `wide`; only after
-// memo_lds_accepted said yes for p32.lds_entries).  fold (diagnostic
-// builds, QSMD_DIAG_FOLD2): the launch is the call's last (no giant launch):
-// its last workgroup out finishes the call (totals, probe, counters) with t.
-// start / stop: events the launch records at the kernel's start and end
+// memo_lds_accepted said yes for p32.lds_entries).  start / stop: events
+// the launch records at the kernel's start and end
 hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool lds_tables,
-                       bool fold, const SplitArgs& t, hipStream_t s, hipEvent_t start, hipEvent_t stop);
+                       hipStream_t s, hipEvent_t start, hipEvent_t stop);
 bool memo_lds_accepted(uint32_t model_id, uint32_t lds_entries, size_t cap);
 
 hipError_t launch_gen(const qsmd_gen_params& p, uint64_t first, uint64_t n_hist, uint32_t ev_base, qsmd_hdr* hdr,

@@ -29,19 +29,7 @@
 
 #include "internal.h"
 #include "lane.h"
-#include "split.h"
 
-// QSMD_DIAG_FOLD2=1 (diagnostic builds only, tools/build_variant.sh): the
-// folded tail that also takes the giant launch's place (fold 2), without a
-// giant fallback -- the whole giant stage in this kernel would cost it its
-// register budget (248 VGPRs: occupancy 1 instead of 4), so a call with
-// giants is left unsearched there (flagged through the time-limit word)
-#ifndef QSMD_DIAG_FOLD2
-#define QSMD_DIAG_FOLD2 0
-#endif
-#ifndef QSMD_DIAG_MEMOPRIO
-#define QSMD_DIAG_MEMOPRIO 0
-#endif
 
 namespace qsmd {
 
@@ -108,11 +96,16 @@ __device__ __forceinline__ LaneKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d
 template <uint32_t MODEL, class G>
 __device__ __forceinline__ bool memo_lookup(const uint32_t* tab, const LaneKey<MODEL, G>& k, uint32_t h,
                                             uint32_t& count) {
+    // the whole entry in one round trip: both 16-B loads issued before any
+    // compare (with && the compiler loaded word 0, compared, then the rest,
+    // then the count -- two or three dependent HBM round trips per probe)
     const uint4* e = reinterpret_cast<const uint4*>(tab + (uint64_t)k.slot * MemoEntry<G>::W);
-    const uint4 x0 = e[0], x1 = e[1];
-    bool hit = x0.x == h && x0.y == k.w1 && x0.z == k.rem_lo && x1.x == k.m[0] && x1.y == k.m[1] &&
-               x1.z == k.m[2] && x1.w == k.m[3];
-    if constexpr (G::EV == 64) hit = hit && e[2].x == k.rem_hi;
+    uint4 x0 = e[0], x1 = e[1];
+    asm volatile("" : "+v"(x0.x), "+v"(x0.y), "+v"(x0.z), "+v"(x0.w), "+v"(x1.x), "+v"(x1.y), "+v"(x1.z),
+                 "+v"(x1.w));
+    bool hit = (x0.x == h) & (x0.y == k.w1) & (x0.z == k.rem_lo) & (x1.x == k.m[0]) & (x1.y == k.m[1]) &
+               (x1.z == k.m[2]) & (x1.w == k.m[3]);
+    if constexpr (G::EV == 64) hit = hit & (e[2].x == k.rem_hi);
     count = x0.w;
     return hit;
 }
@@ -138,10 +131,11 @@ constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
 template <uint32_t MODEL, class G>
 __device__ __forceinline__ bool memo_lookup_lds(const uint32_t* col, const LaneKey<MODEL, G>& k, uint32_t h,
                                                 uint32_t& count) {
+    // every word read before any compare (one LDS round trip, see memo_lookup)
     const uint32_t* e = col + k.slot * 8u * C_LANES;
-    bool hit = e[0] == h && e[1 * C_LANES] == k.w1 && e[2 * C_LANES] == k.rem_lo && e[4 * C_LANES] == k.m[0];
+    bool hit = (e[0] == h) & (e[1 * C_LANES] == k.w1) & (e[2 * C_LANES] == k.rem_lo) & (e[4 * C_LANES] == k.m[0]);
     if constexpr (MODEL == QSMD_MODEL_BANK)
-        hit = hit && e[5 * C_LANES] == k.m[1] && e[6 * C_LANES] == k.m[2] && e[7 * C_LANES] == k.m[3];
+        hit = hit & (e[5 * C_LANES] == k.m[1]) & (e[6 * C_LANES] == k.m[2]) & (e[7 * C_LANES] == k.m[3]);
     count = e[3 * C_LANES];
     return hit;
 }
@@ -363,19 +357,12 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
 // G32 memo tables in LDS after the group (a short list: the heavy stage's
 // time is one search's DFS chain, and the HBM probe was half of it).
 //
-// With the folded tail (api.hip fold0w: the last call deferred nothing) no
+// With the folded tail (api.hip fold: the last call deferred nothing) no
 // stage 0w runs: p64's list is stage 0's deferred list, which without `wide`
-// goes on to the giant list.  fold (diagnostic builds, QSMD_DIAG_FOLD2): the
-// launch is also the call's last -- the last workgroup out (a ticket on
-// C_MEXIT) finishes the call (totals, probe, counters) instead of the giant
-// launch.
+// goes on to the giant list.
 template <uint32_t MODEL, bool LT>
-__global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(SplitArgs t, MemoArgs p32, MemoArgs p64,
-                                                                   uint32_t wide, uint32_t fold) {
+__global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32, MemoArgs p64, uint32_t wide) {
     extern __shared__ uint32_t lds[];
-#if QSMD_DIAG_MEMOPRIO
-    __builtin_amdgcn_s_setprio(QSMD_DIAG_MEMOPRIO);   // diagnostic builds: issue priority over stage 0's waves
-#endif
     const int lane = threadIdx.x;
     const uint64_t n32 = (list_total(p32.s.list_count, p32.s.list_shard_cap) + 63u) / 64u,
                    n64 = (list_total(p64.s.list_count, p64.s.list_shard_cap) + 63u) / 64u;
@@ -410,30 +397,6 @@ __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(SplitArgs t, 
         }
     }
     cnt.flush(p32.s.buckets, lane);
-#if QSMD_DIAG_FOLD2
-    if (fold) {
-        // the last workgroup out: every other one has stored its results and
-        // counts (drained, then released with the ticket)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        uint32_t last = 0;
-        if (lane == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            last = atomicAdd(t.cnt + C_MEXIT, 1u) == gridDim.x - 1u;
-        }
-        if (__shfl(last, 0, 64)) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (ld_cnt(t.cnt + C_GIANT) != 0u) {
-                if (t.probe_host && lane == 0) t.probe_host[kProbeFold] = 1u;
-                if (lane == 0) atomicOr(t.s.timed_out, 4u);
-            }
-            finish_call(t, lane);
-        }
-    }
-#else
-    (void)fold;
-#endif
 }
 
 template <uint32_t MODEL>
@@ -442,12 +405,12 @@ static size_t memo_lds_bytes(uint32_t lds_entries) {
 }
 
 template <uint32_t MODEL, bool LT>
-static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool fold,
-                                const SplitArgs& t, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+static hipError_t launch_memo_t(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, hipStream_t s,
+                                hipEvent_t start, hipEvent_t stop) {
     const size_t lds = LT ? memo_lds_bytes<MODEL>(p32.lds_entries)
                           : (wide ? sizeof(MemoLds<MODEL, G64>) : sizeof(MemoLds<MODEL, G32>));
-    hipExtLaunchKernelGGL((memo_search<MODEL, LT>), dim3(grid), dim3(C_LANES), lds, s, start, stop, 0u, t, p32, p64,
-                          wide ? 1u : 0u, fold ? 1u : 0u);
+    hipExtLaunchKernelGGL((memo_search<MODEL, LT>), dim3(grid), dim3(C_LANES), lds, s, start, stop, 0u, p32, p64,
+                          wide ? 1u : 0u);
     return hipGetLastError();
 }
 
@@ -472,13 +435,13 @@ bool memo_lds_accepted(uint32_t model_id, uint32_t lds_entries, size_t cap) {
 
 // lds_tables (with !wide): the caller has checked memo_lds_accepted
 hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool lds_tables,
-                       bool fold, const SplitArgs& t, hipStream_t s, hipEvent_t start, hipEvent_t stop) {
+                       hipStream_t s, hipEvent_t start, hipEvent_t stop) {
     const bool bank = p32.s.model_id == QSMD_MODEL_BANK;
     if (lds_tables && !wide)
-        return bank ? launch_memo_t<QSMD_MODEL_BANK, true>(p32, p64, grid, wide, fold, t, s, start, stop)
-                    : launch_memo_t<QSMD_MODEL_TICKET, true>(p32, p64, grid, wide, fold, t, s, start, stop);
-    return bank ? launch_memo_t<QSMD_MODEL_BANK, false>(p32, p64, grid, wide, fold, t, s, start, stop)
-                : launch_memo_t<QSMD_MODEL_TICKET, false>(p32, p64, grid, wide, fold, t, s, start, stop);
+        return bank ? launch_memo_t<QSMD_MODEL_BANK, true>(p32, p64, grid, wide, s, start, stop)
+                    : launch_memo_t<QSMD_MODEL_TICKET, true>(p32, p64, grid, wide, s, start, stop);
+    return bank ? launch_memo_t<QSMD_MODEL_BANK, false>(p32, p64, grid, wide, s, start, stop)
+                : launch_memo_t<QSMD_MODEL_TICKET, false>(p32, p64, grid, wide, s, start, stop);
 }
 
 }  // namespace qsmd
