@@ -195,13 +195,18 @@ class InFlight:
         # the last (partial) block's runs here, inside the window: the job's
         # only collective is part of what it times (at the driver's 20 steps
         # it is the window's one collective)
+        t_drain = time.perf_counter()
         self.drain()
+        t_sync = time.perf_counter()
         torch.cuda.synchronize(self.dev)
         # each rank's window runs from the common opening barrier to its own
         # GPU's end; the MAX over ranks below is the whole job's time, so the
         # closing barrier stays outside the window (inside it, its ~137 us of
         # host gloo round trips were ~5 % of a 20-step run)
         elapsed = time.perf_counter() - t0
+        if os.environ.get("QSMD_BENCH_HOSTTIME") == "1":   # where the window's host time goes
+            print(json.dumps({"enqueue_ms": (t_drain - t0) * 1e3, "drain_ms": (t_sync - t_drain) * 1e3,
+                              "sync_ms": (t0 + elapsed - t_sync) * 1e3}), file=sys.stderr)
         for c in self.ctxs:
             c.set_param("timing_events", 1)
         torch.cuda.synchronize(self.dev)

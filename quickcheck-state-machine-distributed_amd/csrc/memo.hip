@@ -305,16 +305,39 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
     }
     if (search) {
         bool skip = false;
-        uint32_t iter = 0;
-        do {
-            const bool was = skip;
-            status = memo_step<MODEL, G, LT>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch, mask,
-                                                 &L.entry[0][lane], skip, p.memo_after);
-            if constexpr (ST) hits += (!was && skip) ? 1u : 0u;
-            ++iter;
-            if (p.giant_cap && iter >= p.giant_cap && status < 0) {
-                status = QSMD_STATUS_HANDED_OFF;
-            } else if ((iter & 1023u) == 0u && status < 0) {
+        // the iteration count is the wavefront's (its lanes start together and
+        // a lane steps in every iteration until it stops), so the hand-off
+        // cap and the checks every 1024 iterations sit outside the inner loop
+        uint64_t iter = 0;
+        const uint64_t cap = p.giant_cap ? p.giant_cap : ~0ull;
+        uint32_t lane_iter = 0;   // (ST only)
+        // nothing outstanding at the loop's entry: otherwise the compiler
+        // waits for the memo insert's stores inside the loop (vmcnt counts
+        // them), a store round trip on every backtrack
+        __builtin_amdgcn_s_waitcnt(0);
+        while (true) {
+            const uint64_t span = cap - iter < 1024u ? cap - iter : 1024u;
+            uint64_t k = 0;
+            while (k < span) {
+                if (status < 0) {
+                    const bool was = skip;
+                    status = memo_step<MODEL, G, LT>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch,
+                                                     mask, &L.entry[0][lane], skip, p.memo_after);
+                    if constexpr (ST) {
+                        hits += (!was && skip) ? 1u : 0u;
+                        ++lane_iter;
+                    }
+                }
+                ++k;
+                if (__ballot(status < 0) == 0ull) break;
+            }
+            iter += k;
+            if (__ballot(status < 0) == 0ull) break;
+            if (iter >= cap) {
+                if (status < 0) status = QSMD_STATUS_HANDED_OFF;
+                break;
+            }
+            if (status < 0) {   // every 1024 iterations
                 if (beyond_first_fail(a, h)) {
                     status = QSMD_STATUS_SKIPPED;
                 } else if (a.time_limit && __builtin_amdgcn_s_memrealtime() - t0 > a.time_limit) {
@@ -322,10 +345,10 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
                     status = QSMD_STATUS_BUDGET;
                 }
             }
-        } while (status < 0);
+        }
         if constexpr (ST) {
-            atomicMax(q + 3, (unsigned long long)iter);
-            atomicAdd(q + 4, (unsigned long long)iter);
+            atomicMax(q + 3, (unsigned long long)lane_iter);
+            atomicAdd(q + 4, (unsigned long long)lane_iter);
             atomicAdd(q + 5, (unsigned long long)hits);
             atomicMax(q + 7, (unsigned long long)(__builtin_amdgcn_s_memtime() - c0));
         }
