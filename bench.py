@@ -181,6 +181,8 @@ class InFlight:
         self.drain()
         torch.cuda.synchronize(self.dev)
         self.done = [None, None]               # (the warm-up's collectives are complete: no waits on them)
+        if os.environ.get("QSMD_BENCH_NOAR_WINDOW") == "1":   # diagnostic: the communicator, no collective in the window
+            self.do_ar = False
         if self.use_dist:
             dist.barrier(group=self.host_group)
         torch.cuda.synchronize(self.dev)

@@ -184,8 +184,10 @@ int qsmd_check_batch(qsmd_ctx* ctx, uint32_t model_id,
                      uint8_t* witness_out, qsmd_totals* totals_out);
 
 /* Same, with every buffer already resident in device memory (HBM) and work
- * enqueued on `stream` (a hipStream_t, NULL = the context's stream): two to
- * four kernel launches, no host round trip.  totals_dev (device, may be NULL)
+ * enqueued on `stream` (a hipStream_t, NULL = the context's stream, a
+ * blocking stream: ordered after the caller's work on the legacy default
+ * stream, as HIP orders blocking streams): two to five kernel launches, no
+ * host round trip.  totals_dev (device, may be NULL)
  * receives the qsmd_totals of the batch.  Asynchronous: synchronise the
  * stream before reading outputs. */
 int qsmd_check_batch_device(qsmd_ctx* ctx, uint32_t model_id,

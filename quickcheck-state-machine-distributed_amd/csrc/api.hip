@@ -171,9 +171,12 @@ int fail(qsmd_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
 // The context's own stream (host entry points, device calls given no
 // stream), created on first use: a caller that always passes its streams
 // (bench.py's calls in flight) leaves no idle stream sharing the device's
-// hardware queues with the ones it uses.
+// hardware queues with the ones it uses.  A blocking stream: a caller that
+// passes NULL (torch's default stream is handle 0) gets its calls ordered
+// after the work it enqueued on the legacy default stream (a fill or copy of
+// the inputs), as HIP orders any blocking stream with that one.
 hipStream_t ctx_stream(qsmd_ctx* c) {
-    if (!c->stream && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (!c->stream && hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess) {
         (void)hipGetLastError();
         c->stream = nullptr;
     }
