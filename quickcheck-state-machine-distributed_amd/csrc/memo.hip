@@ -155,6 +155,19 @@ __device__ __forceinline__ void memo_insert_lds(uint32_t* col, const LaneKey<MOD
     }
 }
 
+// The slots this lane has written for its current history, as 64 bits
+// (slot & 63: a set bit means "maybe written").  An entry can only match
+// when the lane wrote it for this history in this call (the key holds the
+// history index and the call's epoch), so a probe of a clear bit is a miss
+// without the HBM round trip -- most probes: a heavy search finds ~1 % of
+// its states in the table.
+struct Written {
+    uint64_t m;
+    __device__ __forceinline__ void clear() { m = 0ull; }
+    __device__ __forceinline__ void set(uint32_t slot) { m |= 1ull << (slot & 63u); }
+    __device__ __forceinline__ bool maybe(uint32_t slot) const { return (m >> (slot & 63u)) & 1ull; }
+};
+
 // One DFS iteration with the memo (LaneDFS::step plus the two hooks).
 // entry: the lane's column of node counts at entry, per level; tab: the
 // lane's HBM table, or (LT) its LDS column.
@@ -162,7 +175,7 @@ template <uint32_t MODEL, class G, bool LT>
 __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* evc,
                                          int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* tab,
                                          uint32_t h, uint32_t epoch, uint32_t mask, uint32_t* entry, bool& skip,
-                                         uint64_t memo_after) {
+                                         uint64_t memo_after, Written& wr) {
     using M = typename G::M;
     // a short search runs as the plain DFS (no HBM probe per node); the memo
     // joins once the search has counted memo_after nodes (entry counts are
@@ -180,8 +193,12 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
             const uint32_t cnt = (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES];
             const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             if (k.ok) {
-                if constexpr (LT) memo_insert_lds<MODEL, G>(tab, k, h, cnt);
-                else memo_insert<MODEL, G>(tab, k, h, cnt);
+                if constexpr (LT) {
+                    memo_insert_lds<MODEL, G>(tab, k, h, cnt);
+                } else {
+                    memo_insert<MODEL, G>(tab, k, h, cnt);
+                    wr.set(k.slot);
+                }
             }
         }
         skip = false;
@@ -199,9 +216,14 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
             const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
             uint32_t cnt = 0;
             bool hit = false;
-            if (k.ok) {
-                if constexpr (LT) hit = memo_lookup_lds<MODEL, G>(tab, k, h, cnt);
-                else hit = memo_lookup<MODEL, G>(tab, k, h, cnt);
+            if constexpr (LT) {
+                if (k.ok) hit = memo_lookup_lds<MODEL, G>(tab, k, h, cnt);
+            } else {
+#ifndef QSMD_NO_WRITTEN_MAP
+                if (k.ok && wr.maybe(k.slot)) hit = memo_lookup<MODEL, G>(tab, k, h, cnt);
+#else
+                if (k.ok) hit = memo_lookup<MODEL, G>(tab, k, h, cnt);
+#endif
             }
             if (hit) {
                 if (d.nodes + cnt > limit) {      // the budget falls inside that subtree
@@ -311,6 +333,8 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
         uint64_t iter = 0;
         const uint64_t cap = p.giant_cap ? p.giant_cap : ~0ull;
         uint32_t lane_iter = 0;   // (ST only)
+        Written wr;
+        wr.clear();
         // nothing outstanding at the loop's entry: otherwise the compiler
         // waits for the memo insert's stores inside the loop (vmcnt counts
         // them), a store round trip on every backtrack
@@ -322,7 +346,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
                 if (status < 0) {
                     const bool was = skip;
                     status = memo_step<MODEL, G, LT>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch,
-                                                     mask, &L.entry[0][lane], skip, p.memo_after);
+                                                     mask, &L.entry[0][lane], skip, p.memo_after, wr);
                     if constexpr (ST) {
                         hits += (!was && skip) ? 1u : 0u;
                         ++lane_iter;
