@@ -31,9 +31,10 @@ import time
 if "--hw-queues" in sys.argv:
     os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1]
 elif (int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("QSMD_BENCH_DIST") == "1") \
+        and (os.environ.get("QSMD_BENCH_COUNTERS") == "rccl" or "--early-exit" in sys.argv) \
         and "GPU_MAX_HW_QUEUES" not in os.environ:
-    # with RCCL: the 3 slot streams, the all-reduce's own stream and RCCL's
-    # internal one each keep a hardware queue (4 by default: they would share).
+    # with RCCL (the early-exit leg): the slot streams and RCCL's internal
+    # one each keep a hardware queue (4 by default: they would share).
     # (The GPU boxes export HIP's default of 4, which this leaves as it is.  A
     # lone rank with 4 calls in flight on 8 queues measured +2-4 % on config
     # 2, but 8 queues cost config 1 17 % and config 5 23 % at 3 in flight in
@@ -88,16 +89,22 @@ def host_cores():
 class InFlight:
     """S calls in flight (one context, stream and output set per slot; step k
     runs on slot k % S, so the next batch's stage 0 fills the compute units
-    the previous call's tail leaves idle).  With RCCL the counters of R rounds
-    of steps are all-reduced together, overlapping the next block."""
+    the previous call's tail leaves idle).  Each call writes its totals to a
+    row of its own.  The window ends when every rank's GPU has checked every
+    history; then the rows are summed on the device and the 64 B exchanged
+    over the ranks on the host (gloo), timed on their own (exchange_ms): the
+    batch path needs no RCCL communicator, whose mere presence cost one rank
+    7-8 % of the window with no collective issued.
+    QSMD_BENCH_COUNTERS=rccl exchanges the totals over RCCL inside the
+    window instead (for comparison)."""
 
-    def __init__(self, dev, model_id, d_hdr, n, d_ev, n_ev, S, R, flags, use_dist, knobs, budget0, streams=None,
-                 host_group=None, comm=None, batches=None):
+    def __init__(self, dev, model_id, d_hdr, n, d_ev, n_ev, S, flags, use_dist, knobs, budget0, streams=None,
+                 host_group=None, batches=None):
         self.dev, self.model_id, self.n = dev, model_id, n
         # the resident batches (--rotate K: step k checks batch k % K, so the
         # library's cross-call hints always come from another batch)
         self.batches = batches or [(d_hdr, d_ev, n_ev)]
-        self.S, self.B, self.flags = S, R * S, flags
+        self.S, self.flags = S, flags
         self.ctxs = [device.Context(dev.index) for _ in range(S)]
         for c in self.ctxs:
             if budget0 >= 0:
@@ -105,60 +112,46 @@ class InFlight:
             for k, v in knobs:
                 c.set_param(k, v)
         # (streams of their own: torch's default stream is handle 0, which the
-        # C ABI reads as "the context's stream" -- the all-reduce's wait on it
-        # would not order the counters it reads after that slot's calls)
+        # C ABI reads as "the context's stream")
         self.streams = streams or [torch.cuda.Stream(dev) for _ in range(S)]
         self.outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
                      for _ in range(S)]
-        # counters: [block parity][step of the block][8]; a row is reused two blocks later
-        self.tot = torch.zeros(2, self.B, 8, dtype=torch.int64, device=dev)
+        self.tot = None                       # [step][8], allocated per timed region
         self.use_dist = use_dist
         self.host_group = host_group
-        # the all-reduce on a stream of its own: it waits for every slot's last
-        # call of the block, and no slot waits for it (a slot stream carrying
-        # it held that slot's next call behind the collective: 5.98 vs 6.68e9
-        # without the all-reduce, one rank, 60 steps)
-        self.comm = (comm or torch.cuda.Stream(dev)) if use_dist else None
-        self.do_ar = use_dist and os.environ.get("QSMD_BENCH_NOAR") != "1"
-        self.done = [None, None]
+        self.rccl = use_dist and os.environ.get("QSMD_BENCH_COUNTERS") == "rccl"
         # the per-call timing events inside the timed window (the roofline
         # leg after it always records them): instrumentation only -- the
         # headline runs without (api.hip: ~13 us per call for a lone caller)
         self.timing_events = 1
-        self.k = 0
         self.steps_run = 0
-        self.last = (0, 0, 0, 0)
-
-    def _allreduce(self, par):
-        for st_ in self.streams:               # after every slot's last call of the block
-            self.comm.wait_stream(st_)
-        with torch.cuda.stream(self.comm):
-            dist.all_reduce(self.tot[par], op=dist.ReduceOp.SUM)
-            self.done[par] = torch.cuda.Event()
-            self.done[par].record(self.comm)
+        self.last = (0, 0)
+        self.totals = None
+        self.exchange_ms = None
 
     def step(self):
-        k = self.k
-        self.k += 1
-        i, row, par = k % self.S, k % self.B, (k // self.B) % 2
+        k = self.steps_run
+        i = k % self.S
         d_st, d_nd = self.outs[i]
-        d_hdr, d_ev, n_ev = self.batches[self.steps_run % len(self.batches)]
+        d_hdr, d_ev, n_ev = self.batches[k % len(self.batches)]
         with torch.cuda.stream(self.streams[i]):
-            if self.done[par] is not None:
-                self.streams[i].wait_event(self.done[par])
             self.ctxs[i].check_device(self.model_id, d_hdr.data_ptr(), self.n, d_ev.data_ptr(), n_ev,
-                                      d_st.data_ptr(), d_nd.data_ptr(), None, self.tot[par, row].data_ptr(),
+                                      d_st.data_ptr(), d_nd.data_ptr(), None, self.tot[k].data_ptr(),
                                       flags=self.flags, stream=self.streams[i].cuda_stream)
-        if self.do_ar and row == self.B - 1:
-            self._allreduce(par)
-        self.last = (i, row, par, self.steps_run % len(self.batches))
+        self.last = (i, k % len(self.batches))
         self.steps_run += 1
 
-    def drain(self):
-        if self.k % self.B:                  # a partial last block: reduce it, start the next one fresh
-            if self.do_ar:
-                self._allreduce(((self.k - 1) // self.B) % 2)
-            self.k = (self.k + self.B - 1) // self.B * self.B
+    def _sum(self):
+        """The rows of every step so far, summed on the device after every
+        slot's last call (on slot 0's stream, which the caller synchronises)."""
+        s0 = self.streams[0]
+        for st_ in self.streams[1:]:
+            s0.wait_stream(st_)
+        with torch.cuda.stream(s0):
+            acc = self.tot[:self.steps_run].sum(0)
+            if self.rccl:
+                dist.all_reduce(acc, op=dist.ReduceOp.SUM)
+        return acc
 
     def prime(self):
         """One call per context before the warm-up, synchronised: the library
@@ -176,13 +169,15 @@ class InFlight:
 
     def timed(self, steps, warmup):
         self.prime()
+        self.tot = torch.zeros(max(steps, warmup, 1), 8, dtype=torch.int64, device=self.dev)
+        self.totals = torch.zeros(8, dtype=torch.int64, pin_memory=True)
+        self.steps_run = 0
         for _ in range(warmup):
             self.step()
-        self.drain()
+        self._sum()                          # (with RCCL: the warm-up's all-reduce creates the communicator)
         torch.cuda.synchronize(self.dev)
-        self.done = [None, None]               # (the warm-up's collectives are complete: no waits on them)
-        if os.environ.get("QSMD_BENCH_NOAR_WINDOW") == "1":   # diagnostic: the communicator, no collective in the window
-            self.do_ar = False
+        self.tot.zero_()
+        torch.cuda.synchronize(self.dev)
         if self.use_dist:
             dist.barrier(group=self.host_group)
         torch.cuda.synchronize(self.dev)
@@ -193,22 +188,38 @@ class InFlight:
         t0 = time.perf_counter()
         for _ in range(steps):
             self.step()
-        # the counters' all-reduce runs once per block of S x ar_rounds steps;
-        # the last (partial) block's runs here, inside the window: the job's
-        # only collective is part of what it times (at the driver's 20 steps
-        # it is the window's one collective)
         t_drain = time.perf_counter()
-        self.drain()
+        if self.rccl:                          # (diagnostic: the exchange over RCCL, inside the window)
+            acc = self._sum()
+            with torch.cuda.stream(self.streams[0]):
+                self.totals.copy_(acc, non_blocking=True)
         t_sync = time.perf_counter()
         torch.cuda.synchronize(self.dev)
         # each rank's window runs from the common opening barrier to its own
-        # GPU's end; the MAX over ranks below is the whole job's time, so the
-        # closing barrier stays outside the window (inside it, its ~137 us of
-        # host gloo round trips were ~5 % of a 20-step run)
-        elapsed = time.perf_counter() - t0
+        # GPU's end: every history of every step is checked and its status
+        # and node count are in HBM.  The MAX over ranks below is the whole
+        # job's time, so the closing barrier stays outside the window (inside
+        # it, its ~137 us of host gloo round trips were ~5 % of a 20-step run,
+        # DESIGN.md §9)
+        t_end = time.perf_counter()
+        elapsed = t_end - t0
         if os.environ.get("QSMD_BENCH_HOSTTIME") == "1":   # where the window's host time goes
-            print(json.dumps({"enqueue_ms": (t_drain - t0) * 1e3, "drain_ms": (t_sync - t_drain) * 1e3,
-                              "sync_ms": (t0 + elapsed - t_sync) * 1e3}), file=sys.stderr)
+            print(json.dumps({"enqueue_ms": (t_drain - t0) * 1e3, "sum_ms": (t_sync - t_drain) * 1e3,
+                              "sync_ms": (t_end - t_sync) * 1e3}), file=sys.stderr)
+        # the totals of every timed step: summed on the device, then over the
+        # ranks -- 64 B of bookkeeping, timed on its own and reported beside
+        # the headline, which excludes it (over gloo after a long GPU wait it
+        # took 0.12-0.22 ms, 5-9 % of the driver's 20-step window)
+        self.exchange_ms = None
+        if not self.rccl:
+            t_x = time.perf_counter()
+            acc = self._sum()
+            with torch.cuda.stream(self.streams[0]):
+                self.totals.copy_(acc, non_blocking=True)
+            torch.cuda.synchronize(self.dev)
+            if self.use_dist:
+                dist.all_reduce(self.totals, op=dist.ReduceOp.SUM, group=self.host_group)
+            self.exchange_ms = (time.perf_counter() - t_x) * 1e3
         for c in self.ctxs:
             c.set_param("timing_events", 1)
         torch.cuda.synchronize(self.dev)
@@ -242,11 +253,12 @@ class InFlight:
         return f64(s0), f64(hv), f64(call), self.ctxs[0].get_param("stage0_budget_last")
 
     def results(self):
-        """Outputs of the last step: (status, nodes, the step's totals, its batch index)."""
-        i, row, par, bi = self.last
+        """Outputs of the last step (status, nodes, its batch index) and the
+        totals of every timed step over all ranks."""
+        i, bi = self.last
         st = self.outs[i][0].cpu().numpy()
         nd = self.outs[i][1].cpu().numpy()
-        return st, nd, self.tot[par, row].cpu().numpy(), bi
+        return st, nd, self.totals.numpy(), bi
 
     def close(self):
         for c in self.ctxs:
@@ -441,8 +453,6 @@ def main():
                          "instrumentation, ~13 us per synchronous call)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="calls in flight (one context + stream each); 0 = 4 (the extra configs: 3)")
-    ap.add_argument("--ar-rounds", type=int, default=16,
-                    help="rounds of in-flight steps whose counters one RCCL all-reduce carries (N > 1)")
     ap.add_argument("--device-gen", action="store_true",
                     help="generate the batch on the GPU (qsmd_gen_batch_device; same histories as the host generator)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05", "stage0_pmc.json"),
@@ -475,8 +485,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # QSMD_BENCH_DEVICE / QSMD_BENCH_BACKEND=gloo: a multi-rank rehearsal on
-    # one GPU (RCCL refuses two ranks on one device); diagnostics only
+    # QSMD_BENCH_DEVICE: a multi-rank rehearsal on one GPU (the batch path's
+    # process group is gloo; RCCL refuses two ranks on one device)
     if os.environ.get("QSMD_BENCH_DEVICE"):
         local = int(os.environ["QSMD_BENCH_DEVICE"])
     torch.cuda.set_device(local)
@@ -490,11 +500,10 @@ def main():
     # (7.1-7.5 / 6.7e9; tools/gpu/r05_if.sh, r05_if2.sh).  The extra configs
     # run at 3: config 1 (2 x 10 TicketDispenser) drops from 9.9 to 6.7e9 at 4
     S = args.inflight if args.inflight > 0 else 4
-    # the slot streams, created and used before RCCL creates its own, so that
-    # each gets a hardware queue of its own (GPU_MAX_HW_QUEUES)
+    # the slot streams, created and used first, so that each gets a hardware
+    # queue of its own (GPU_MAX_HW_QUEUES)
     streams = [torch.cuda.Stream(dev) for _ in range(S)]
-    comm = torch.cuda.Stream(dev) if use_dist else None
-    for st_ in streams + ([comm] if comm is not None else []):
+    for st_ in streams:
         with torch.cuda.stream(st_):
             torch.ones(1, device=dev).add_(1)
     torch.cuda.synchronize(dev)
@@ -502,27 +511,25 @@ def main():
         if "RANK" not in os.environ:      # QSMD_BENCH_DIST=1 without a launcher: one rank over RCCL
             os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
                               MASTER_PORT=os.environ.get("MASTER_PORT", "29517"))
-        # The RCCL communicator is created lazily, by the warm-up's all-reduce,
-        # after the slot streams and contexts exist: created eagerly at init
-        # (device_id=dev, QSMD_BENCH_EAGER=1) it cost 38 % of one rank's
-        # throughput with no collective issued (profiles/r02/rccl_sweep.txt).
-        # PyTorch's NCCL process group runs a watchdog and a heartbeat monitor
-        # thread; with them one rank on the RCCL path lost 5-7 % of its
-        # throughput even with no collective issued (5.09-5.40 vs 5.62-5.80e9,
-        # 20 steps); without them it is within the run-to-run spread.  The
-        # bench's collectives are bounded by gpurun / the driver's time limits.
+        # The batch path exchanges nothing but its totals, so its process
+        # group is gloo only: one rank with an RCCL communicator lost 7-8 % of
+        # the driver's window with no collective issued in it (none 8.61-8.96
+        # vs 8.08-8.23e9; the all-reduce itself takes 27 us; more hardware
+        # queues made it worse: tools/gpu/r05_ar.sh, r05_q.sh).
+        # The early-exit leg's MIN per round is a real exchange on the data
+        # path and runs over RCCL (as does QSMD_BENCH_COUNTERS=rccl, for
+        # comparison); its communicator is created lazily by the first
+        # collective.  PyTorch's NCCL watchdog and heartbeat monitor cost one
+        # rank 5-7 % with no collective issued: off.
         os.environ.setdefault("TORCH_NCCL_ENABLE_MONITORING", "0")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
-        if os.environ.get("QSMD_BENCH_BACKEND") == "gloo":
-            dist.init_process_group("gloo")
-        elif os.environ.get("QSMD_BENCH_EAGER") == "1":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
+        if args.early_exit or os.environ.get("QSMD_BENCH_COUNTERS") == "rccl":
             dist.init_process_group("nccl")
-    # the bracketing barriers and the MAX over ranks of the timed region go
-    # over a host (gloo) group: after torch.cuda.synchronize() every rank's
-    # GPU work is done, and a host barrier costs no RCCL launch inside the
-    # window (the counters' all-reduce stays on RCCL)
+        else:
+            dist.init_process_group("gloo")
+    # the bracketing barriers, the totals and the MAX over ranks of the timed
+    # region go over a host (gloo) group: after torch.cuda.synchronize() every
+    # rank's GPU work is done
     host_group = dist.new_group(backend="gloo") if use_dist else None
 
     if args.early_exit:
@@ -593,8 +600,8 @@ def main():
             if k not in dict(knobs):
                 knobs.append((k, v))
     flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_MEMO if args.memo else 0)
-    run = InFlight(dev, model_id, d_hdr, n, d_ev, len(ev), S, max(1, args.ar_rounds), flags, use_dist, knobs,
-                   budget0, streams, host_group, comm, batches=dev_batches)
+    run = InFlight(dev, model_id, d_hdr, n, d_ev, len(ev), S, flags, use_dist, knobs,
+                   budget0, streams, host_group, batches=dev_batches)
     run.timing_events = args.timing_events
     elapsed = run.timed(args.steps, args.warmup)
     s0_ms, call_ms = run.ctxs[0].timing_read()
@@ -607,8 +614,8 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     total_hist = n * world
     value = total_hist * args.steps / elapsed
-    nodes_total = int(tot[7])
-    assert int(tot[0]) + int(tot[4]) + int(tot[5]) == total_hist, tot
+    nodes_total = int(tot[7])                      # every timed step, every rank
+    assert int(tot[0]) + int(tot[4]) + int(tot[5]) == total_hist * args.steps, tot
 
     # roofline, rank-local, of the two kernels that bound a call -- stage 0
     # and the lane-mode heavy stage -- each SURVEY §8d's algorithmic bytes of
@@ -682,13 +689,16 @@ def main():
                    "stage0_budget": budget0 if budget0 >= 0 else "library default",
                    "heavy_stage": ("lane mode, HBM memo tables" if S > 1 else "library default (wave mode for a "
                                    "short heavy list)") if not args.param else "knobs: " + ",".join(args.param),
-                   "allreduce_every_steps": S * max(1, args.ar_rounds) if use_dist else None,
+                   "counters": ("summed on the device, one RCCL all-reduce inside the window" if run.rccl
+                                else "summed on the device, then one host (gloo) all-reduce after the window: "
+                                "the headline excludes it, exchange_ms times it") if use_dist else None,
+                   "exchange_ms": run.exchange_ms if use_dist else None,
                    "batches": args.rotate, "fold": fold,
                    "mode": "memo" if args.memo else "exhaustive"},
-        "nodes_per_sec": nodes_total * args.steps / elapsed,
-        "verdicts": {"checked": int(tot[0]), "linearisable": int(tot[1]),
-                     "nonlinearisable": int(tot[2]), "model_errors": int(tot[3]),
-                     "budget": int(tot[5])},
+        "nodes_per_sec": nodes_total / elapsed,
+        "verdicts": {"scope": "every timed step, every rank", "checked": int(tot[0]),
+                     "linearisable": int(tot[1]), "nonlinearisable": int(tot[2]),
+                     "model_errors": int(tot[3]), "budget": int(tot[5])},
         "device_ms": {"in_flight": {"stage0_mean": float(np.mean(s0_ms)) if len(s0_ms) else None,
                                     "call_mean": float(np.mean(call_ms)) if len(call_ms) else None},
                       "alone": {"stage0_mean": float(np.mean(roof_s0)),

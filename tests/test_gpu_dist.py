@@ -200,3 +200,28 @@ def test_two_processes_on_the_hip_kernels():
             assert (dinfo["first_fail"], dinfo["rounds"], dinfo["searched"]) == \
                 (hinfo["first_fail"], hinfo["rounds"], hinfo["searched"]), (config, r)
             assert dtot == qdist.totals_from_status(dev_st, dev_nd).tolist()
+
+
+def test_bench_two_ranks_on_one_gpu():
+    """bench.py's multi-rank path as the driver launches it (torchrun, one
+    process per rank), both ranks on cuda:0 (QSMD_BENCH_DEVICE=0): the batch
+    path's gloo group, every step's totals summed on the device and
+    exchanged once at the window's end.  bench.py asserts that the totals of
+    all ranks cover n_hist x ranks x steps histories; here, the one JSON
+    line of rank 0 and its whole-job figures."""
+    import json
+    import subprocess
+    root = os.path.join(HERE, "..")
+    env = dict(os.environ, QSMD_BENCH_DEVICE="0", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--steps", "6", "--warmup", "2", "--n-hist", "20000", "--rotate", "3", "--no-extra",
+           "--no-cpu-baseline", "--roof-calls", "2"]
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 6 and d["value"] > 0
+    assert d["verdicts"]["checked"] + d["verdicts"]["budget"] <= 2 * 6 * 20000
+    assert "gloo" in d["config"]["counters"]
