@@ -393,7 +393,7 @@ def extra_configs(dev, S, knobs, streams):
         hdr, ev, d_hdr, d_ev = device_batch(name, 0, n, dev)
         mid = gen.CONFIGS[name]["model_id"]
         # (the headline's slot streams: the same streams on the same hardware queues)
-        run = InFlight(dev, mid, d_hdr, n, d_ev, len(ev), S, 1, device.QSMD_FLAG_EXHAUSTIVE, False, knobs, -1,
+        run = InFlight(dev, mid, d_hdr, n, d_ev, len(ev), S, device.QSMD_FLAG_EXHAUSTIVE, False, knobs, -1,
                        streams=streams)
         el = run.timed(steps, 3)
         st, nd, tot, _ = run.results()
@@ -403,8 +403,8 @@ def extra_configs(dev, S, knobs, streams):
         st_o, nd_o, _ = oracle_c.check_batch(mid, hdr[:m], ev, threads=host_cores(), max_nodes=0)
         out[f"config{cfg_id}"] = {
             "workload": name, "histories": n, "steps": steps, "histories_per_sec": n * steps / el,
-            "nodes_per_sec": float(tot[7]) * steps / el, "device_ms_call_mean": float(np.mean(call)),
-            "nonlinearisable": int(tot[2]), "mismatches_vs_oracle": int(((st[:m] != st_o) |
+            "nodes_per_sec": float(tot[7]) / el, "device_ms_call_mean": float(np.mean(call)),
+            "nonlinearisable": int(tot[2]) // steps, "mismatches_vs_oracle": int(((st[:m] != st_o) |
                                                                         (nd[:m] != nd_o.astype(np.int64))).sum()),
             "checked_vs_oracle": m}
     h, e, _ = gen.adversarial_ticket(8, 64, bug=True)
