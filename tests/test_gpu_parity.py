@@ -795,3 +795,38 @@ def test_host_waits_stay_with_the_context():
     finally:
         A.close()
         B.close()
+
+
+def test_packed_lookalike_layouts(ctx):
+    """Batches with n_events == 32 n_hist that are NOT one packed block of
+    32-event histories in header order come out as the oracle's: mixed
+    lengths, permuted headers, shorter histories with trailing events, every
+    header pointing one block on, and a partial last group.  (Round 5 built a
+    speculative first staging step keyed on n_events / n_hist -- measured no
+    faster, removed, DESIGN.md §10 -- and these are the layouts it had to
+    reject.)"""
+    rng = random.Random(31)
+    hdr, ev, _ = gen.generate_config("bank_4x16", 77, 64 * 40 + 19)      # packed 32-event histories
+    n = len(hdr)
+    assert len(ev) == 32 * n
+    _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**7)            # as laid out (partial last group)
+    rot = hdr.copy()                                                      # each header points one block on
+    rot["ev_off"] = (np.arange(n, dtype=np.int64) + 1) % n * 32
+    for i in range(n):                                                    # (the history that was there)
+        rot[i]["n_ev"], rot[i]["n_pid"] = hdr[(i + 1) % n]["n_ev"], hdr[(i + 1) % n]["n_pid"]
+    _compare(ctx, models.MODEL_BANK, rot, ev, max_nodes=10**7)
+    perm = hdr[np.random.default_rng(5).permutation(n)]                   # permuted headers
+    _compare(ctx, models.MODEL_BANK, perm, ev, max_nodes=10**7)
+    hs = [histgen.wellformed_history(rng, "bank", 8, rng.randint(1, 4), p_pending=0.0)[:16] for _ in range(2000)]
+    short = codec.encode(models.BANK, hs)                                 # <= 16 events each, then padding
+    pad = np.zeros(32 * len(short.hdr) - len(short.events), dtype=short.events.dtype)
+    _compare(ctx, models.MODEL_BANK, short.hdr, np.concatenate([short.events, pad]), max_nodes=10**7)
+    hs = []
+    while len(hs) < 64 * 20:                                              # 28 / 36 alternating: 32 on average
+        k = 28 if len(hs) % 2 == 0 else 36
+        h = histgen.wellformed_history(rng, "bank", k // 2 + 2, rng.randint(1, 4), p_pending=0.0)
+        if len(h) >= k:
+            hs.append(h[:k])
+    mixed = codec.encode(models.BANK, hs)
+    assert len(mixed.events) == 32 * len(mixed.hdr)
+    _compare(ctx, models.MODEL_BANK, mixed.hdr, mixed.events, max_nodes=10**7)
