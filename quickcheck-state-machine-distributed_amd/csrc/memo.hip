@@ -189,10 +189,13 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     if (empty & !term) {
         // leaving the node at depth d.depth: its subtree was searched to the end and failed
         // (counts kept mod 2^32: exact while the running count is below 2^32)
-        if (memo && !skip && d.nodes <= 0xFFFFFFFFull && entry[(d.depth - 1u) * C_LANES] != kNoEntry) {
-            const uint32_t cnt = (uint32_t)d.nodes - entry[(d.depth - 1u) * C_LANES];
+        // (the level's entry count and the key's balances read together:
+        // gating the key on the entry count put its LDS round trip first)
+        const uint32_t ent = entry[(d.depth - 1u) * C_LANES];
+        if (memo && !skip && d.nodes <= 0xFFFFFFFFull) {
             const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
-            if (k.ok) {
+            const uint32_t cnt = (uint32_t)d.nodes - ent;
+            if (k.ok && ent != kNoEntry) {
                 if constexpr (LT) {
                     memo_insert_lds<MODEL, G>(tab, k, h, cnt);
                 } else {
