@@ -5,9 +5,17 @@ BASELINE.json config 2 -- 1M synthetic 4-client x 16-op Bank histories per GPU
 stream; the histories are independent).
 
 One step = one full pass of the hot path (the linearisability search,
-src/Linearisability.hs:52-69) over the resident batch + the RCCL all-reduce of
-the verdict/node counters (the only collective).  Inputs are resident in HBM
-before the timed region.
+src/Linearisability.hs:52-69) over one resident batch (--rotate K: K
+distinct batches in turn).  Inputs are resident in HBM before the timed
+region.  With N > 1 the ranks exchange nothing during the steps; each step's
+verdict / node counters stay on its GPU, and their sum over the ranks (64 B,
+gloo) follows the window, timed on its own (config.exchange_ms).
+
+Environment (diagnostics): QSMD_BENCH_DIST=1 runs one rank on the N > 1
+path; QSMD_BENCH_COUNTERS=rccl exchanges the counters over RCCL inside the
+window instead; QSMD_BENCH_HOSTTIME=1 prints the window's host-time split
+on stderr; QSMD_BENCH_DEVICE=d pins every rank to GPU d; QSMD_LIB_PATH
+loads another build of libqsmd.so.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
