@@ -8,12 +8,12 @@ One step = one full pass of the hot path (the linearisability search,
 src/Linearisability.hs:52-69) over one resident batch (--rotate K: K
 distinct batches in turn).  Inputs are resident in HBM before the timed
 region.  With N > 1 the ranks exchange nothing during the steps; each step's
-verdict / node counters stay on its GPU, and their sum over the ranks (64 B,
-gloo) follows the window, timed on its own (config.exchange_ms).
+verdict / node counters stay on its GPU, and their RCCL all-reduce over the
+ranks (64 B) follows the window, timed on its own (config.exchange_ms).
 
 Environment (diagnostics): QSMD_BENCH_DIST=1 runs one rank on the N > 1
 path; QSMD_BENCH_COUNTERS=rccl exchanges the counters over RCCL inside the
-window instead; QSMD_BENCH_HOSTTIME=1 prints the window's host-time split
+window instead, =gloo on the host after it; QSMD_BENCH_HOSTTIME=1 prints the window's host-time split
 on stderr; QSMD_BENCH_DEVICE=d pins every rank to GPU d; QSMD_LIB_PATH
 loads another build of libqsmd.so.
 
@@ -99,12 +99,13 @@ class InFlight:
     runs on slot k % S, so the next batch's stage 0 fills the compute units
     the previous call's tail leaves idle).  Each call writes its totals to a
     row of its own.  The window ends when every rank's GPU has checked every
-    history; then the rows are summed on the device and the 64 B exchanged
-    over the ranks on the host (gloo), timed on their own (exchange_ms): the
-    batch path needs no RCCL communicator, whose mere presence cost one rank
-    7-8 % of the window with no collective issued.
-    QSMD_BENCH_COUNTERS=rccl exchanges the totals over RCCL inside the
-    window instead (for comparison)."""
+    history; then the rows are summed on the device and all-reduced over
+    the ranks with RCCL (the verdict / node counters of SURVEY.md §8e), timed
+    on their own (exchange_ms).  The RCCL communicator is created only then:
+    its mere presence cost one rank 7-8 % of the window with no collective
+    issued.  QSMD_BENCH_COUNTERS: "rccl-after" (the default),
+    "rccl" (the communicator from the warm-up, the all-reduce inside the
+    window), "gloo" (the 64 B summed on the host after the window)."""
 
     def __init__(self, dev, model_id, d_hdr, n, d_ev, n_ev, S, flags, use_dist, knobs, budget0, streams=None,
                  host_group=None, batches=None):
@@ -127,7 +128,10 @@ class InFlight:
         self.tot = None                       # [step][8], allocated per timed region
         self.use_dist = use_dist
         self.host_group = host_group
-        self.rccl = use_dist and os.environ.get("QSMD_BENCH_COUNTERS") == "rccl"
+        self.counters = os.environ.get("QSMD_BENCH_COUNTERS", "rccl-after") if use_dist else "none"
+        if self.counters not in ("rccl-after", "rccl", "gloo", "none"):
+            raise SystemExit(f"QSMD_BENCH_COUNTERS={self.counters}: rccl-after, rccl or gloo")
+        self.rccl = self.counters == "rccl"     # (the all-reduce inside the window)
         # the per-call timing events inside the timed window (the roofline
         # leg after it always records them): instrumentation only -- the
         # headline runs without (api.hip: ~13 us per call for a lone caller)
@@ -149,15 +153,16 @@ class InFlight:
         self.last = (i, k % len(self.batches))
         self.steps_run += 1
 
-    def _sum(self):
+    def _sum(self, rccl=False):
         """The rows of every step so far, summed on the device after every
-        slot's last call (on slot 0's stream, which the caller synchronises)."""
+        slot's last call (on slot 0's stream, which the caller synchronises),
+        then over the ranks with RCCL when `rccl`."""
         s0 = self.streams[0]
         for st_ in self.streams[1:]:
             s0.wait_stream(st_)
         with torch.cuda.stream(s0):
             acc = self.tot[:self.steps_run].sum(0)
-            if self.rccl:
+            if rccl:
                 dist.all_reduce(acc, op=dist.ReduceOp.SUM)
         return acc
 
@@ -182,7 +187,7 @@ class InFlight:
         self.steps_run = 0
         for _ in range(warmup):
             self.step()
-        self._sum()                          # (with RCCL: the warm-up's all-reduce creates the communicator)
+        self._sum(self.rccl)                 # ("rccl": the warm-up's all-reduce creates the communicator)
         torch.cuda.synchronize(self.dev)
         self.tot.zero_()
         torch.cuda.synchronize(self.dev)
@@ -198,7 +203,7 @@ class InFlight:
             self.step()
         t_drain = time.perf_counter()
         if self.rccl:                          # (diagnostic: the exchange over RCCL, inside the window)
-            acc = self._sum()
+            acc = self._sum(True)
             with torch.cuda.stream(self.streams[0]):
                 self.totals.copy_(acc, non_blocking=True)
         t_sync = time.perf_counter()
@@ -216,16 +221,19 @@ class InFlight:
                               "sync_ms": (t_end - t_sync) * 1e3}), file=sys.stderr)
         # the totals of every timed step: summed on the device, then over the
         # ranks -- 64 B of bookkeeping, timed on its own and reported beside
-        # the headline, which excludes it (over gloo after a long GPU wait it
-        # took 0.12-0.22 ms, 5-9 % of the driver's 20-step window)
+        # the headline, which excludes it
         self.exchange_ms = None
         if not self.rccl:
+            if self.counters == "rccl-after":   # (the communicator, created now, outside the timing)
+                with torch.cuda.stream(self.streams[0]):
+                    dist.all_reduce(torch.zeros(1, dtype=torch.int64, device=self.dev))
+                torch.cuda.synchronize(self.dev)
             t_x = time.perf_counter()
-            acc = self._sum()
+            acc = self._sum(self.counters == "rccl-after")
             with torch.cuda.stream(self.streams[0]):
                 self.totals.copy_(acc, non_blocking=True)
             torch.cuda.synchronize(self.dev)
-            if self.use_dist:
+            if self.counters == "gloo":
                 dist.all_reduce(self.totals, op=dist.ReduceOp.SUM, group=self.host_group)
             self.exchange_ms = (time.perf_counter() - t_x) * 1e3
         for c in self.ctxs:
@@ -519,22 +527,21 @@ def main():
         if "RANK" not in os.environ:      # QSMD_BENCH_DIST=1 without a launcher: one rank over RCCL
             os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1",
                               MASTER_PORT=os.environ.get("MASTER_PORT", "29517"))
-        # The batch path exchanges nothing but its totals, so its process
-        # group is gloo only: one rank with an RCCL communicator lost 7-8 % of
-        # the driver's window with no collective issued in it (none 8.61-8.96
-        # vs 8.08-8.23e9; the all-reduce itself takes 27 us; more hardware
-        # queues made it worse: tools/gpu/r05_ar.sh, r05_q.sh).
-        # The early-exit leg's MIN per round is a real exchange on the data
-        # path and runs over RCCL (as does QSMD_BENCH_COUNTERS=rccl, for
-        # comparison); its communicator is created lazily by the first
-        # collective.  PyTorch's NCCL watchdog and heartbeat monitor cost one
-        # rank 5-7 % with no collective issued: off.
+        # The RCCL communicator is created lazily by the first collective:
+        # on the batch path after the timed window, since one rank with a
+        # communicator lost 7-8 % of the driver's window with no collective
+        # issued in it (none 8.61-8.96 vs 8.08-8.23e9; the all-reduce itself
+        # takes 27 us; more hardware queues made it worse: tools/gpu/r05_ar.sh,
+        # r05_q.sh).  The early-exit leg's MIN per round is a
+        # real exchange on the data path and creates it in its warm-up.
+        # PyTorch's NCCL watchdog and heartbeat monitor cost one rank 5-7 %
+        # with no collective issued: off.
         os.environ.setdefault("TORCH_NCCL_ENABLE_MONITORING", "0")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
-        if args.early_exit or os.environ.get("QSMD_BENCH_COUNTERS") == "rccl":
-            dist.init_process_group("nccl")
-        else:
+        if os.environ.get("QSMD_BENCH_COUNTERS") == "gloo" and not args.early_exit:
             dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl")
     # the bracketing barriers, the totals and the MAX over ranks of the timed
     # region go over a host (gloo) group: after torch.cuda.synchronize() every
     # rank's GPU work is done
@@ -697,9 +704,13 @@ def main():
                    "stage0_budget": budget0 if budget0 >= 0 else "library default",
                    "heavy_stage": ("lane mode, HBM memo tables" if S > 1 else "library default (wave mode for a "
                                    "short heavy list)") if not args.param else "knobs: " + ",".join(args.param),
-                   "counters": ("summed on the device, one RCCL all-reduce inside the window" if run.rccl
-                                else "summed on the device, then one host (gloo) all-reduce after the window: "
-                                "the headline excludes it, exchange_ms times it") if use_dist else None,
+                   "counters": {"rccl": "summed on the device, one RCCL all-reduce inside the window",
+                                "rccl-after": "summed on the device, one RCCL all-reduce after the window (the "
+                                              "communicator created then): the headline excludes it, exchange_ms "
+                                              "times it",
+                                "gloo": "summed on the device, one host (gloo) all-reduce after the window: the "
+                                        "headline excludes it, exchange_ms times it"}.get(run.counters)
+                   if use_dist else None,
                    "exchange_ms": run.exchange_ms if use_dist else None,
                    "batches": args.rotate, "fold": fold,
                    "mode": "memo" if args.memo else "exhaustive"},
