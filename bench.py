@@ -513,7 +513,7 @@ def main():
     # the pipeline's critical path, and a fourth stream overlaps it -- config
     # 2 at the driver's 20 steps 8.47-8.91e9 against 7.88-8.50e9 with 3 (5
     # alternating rounds), 5 or 6 in flight share hardware queues and lose
-    # (7.1-7.5 / 6.7e9; tools/gpu/r05_if.sh, r05_if2.sh).  The extra configs
+    # (7.1-7.5 / 6.7e9; tools/gpu/archive/r05_if.sh, r05_if2.sh).  The extra configs
     # run at 3: config 1 (2 x 10 TicketDispenser) drops from 9.9 to 6.7e9 at 4
     S = args.inflight if args.inflight > 0 else 4
     # the slot streams, created and used first, so that each gets a hardware
@@ -531,7 +531,7 @@ def main():
         # on the batch path after the timed window, since one rank with a
         # communicator lost 7-8 % of the driver's window with no collective
         # issued in it (none 8.61-8.96 vs 8.08-8.23e9; the all-reduce itself
-        # takes 27 us; more hardware queues made it worse: tools/gpu/r05_ar.sh,
+        # takes 27 us; more hardware queues made it worse: tools/gpu/archive/r05_ar.sh,
         # r05_q.sh).  The early-exit leg's MIN per round is a
         # real exchange on the data path and creates it in its warm-up.
         # PyTorch's NCCL watchdog and heartbeat monitor cost one rank 5-7 %

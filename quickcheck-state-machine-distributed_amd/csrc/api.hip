@@ -552,7 +552,7 @@ static bool lane_tables(qsmd_ctx* c, hipStream_t s, uint64_t grid) {
     // stream of distinct batches moves it a little every call -- sized to
     // the count alone, the tables grew, were cleared and waited for the
     // context's last call in the middle of a caller's stream of calls:
-    // 4.8 vs 8.8e9 histories/s over five resident batches, tools/gpu/r05_rot2.sh)
+    // 4.8 vs 8.8e9 histories/s over five resident batches, tools/gpu/archive/r05_rot2.sh)
     if (grow(c, &c->mt, &c->mt_bytes, need + need / 2, &re) != QSMD_OK &&
         grow(c, &c->mt, &c->mt_bytes, need, &re) != QSMD_OK) {
         (void)hipGetLastError();

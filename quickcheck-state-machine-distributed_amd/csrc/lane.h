@@ -317,7 +317,7 @@ __device__ __forceinline__ void stage_packed_body(const SearchArgs& a, uint32_t 
                 // non-temporal: the events are read once per call (they
                 // need not displace the memo tables and saved states in L2;
                 // the driver's command 8.66 vs 8.63e9 over 8 rounds, 200
-                // steps 9.87-9.93 vs 9.83-9.89e9, tools/gpu/r05_nt.sh)
+                // steps 9.87-9.93 vs 9.83-9.89e9, tools/gpu/archive/r05_nt.sh)
                 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
                 if (!GUARD || q < nq) {
                     const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(&blk[q]));
