@@ -337,7 +337,8 @@ def reference_shaped(seconds):
                       f"oracle/linearise_lists.py (literal list transliteration, CPython)"}
 
 
-def early_exit_leg(dev, rank, world, config, n_per_gpu, steps, warmup, chunk, use_dist, host_group, check_oracle):
+def early_exit_leg(dev, rank, world, config, n_per_gpu, steps, warmup, chunk, use_dist, host_group, check_oracle,
+                   first_chunk=None):
     """BASELINE config 3's early-termination path: QSMD_FLAG_EARLY_EXIT_BATCH
     over a batch sharded across the ranks (qsmd.dist.check_shard_early_exit_device:
     device-resident shards, one MIN all-reduce of the first failure per
@@ -356,7 +357,7 @@ def early_exit_leg(dev, rank, world, config, n_per_gpu, steps, warmup, chunk, us
     mid = gen.CONFIGS[config]["model_id"]
     ctx = device.Context(dev.index)
     run = lambda: qdist.check_shard_early_exit_device(ctx, mid, d_hdr, d_ev, len(ev), n_total, rank, world,  # noqa
-                                                      chunk=chunk, group=None)
+                                                      chunk=chunk, group=None, first_chunk=first_chunk)
     for _ in range(warmup):
         run()
     torch.cuda.synchronize(dev)
@@ -376,7 +377,8 @@ def early_exit_leg(dev, rank, world, config, n_per_gpu, steps, warmup, chunk, us
         s = e[1:].clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM, group=host_group)
         el, searched = float(e[0].item()), int(s.item())
-    out = {"workload": config, "histories": n_total, "histories_per_gpu": n_per_gpu, "chunk": chunk, "steps": steps,
+    out = {"workload": config, "histories": n_total, "histories_per_gpu": n_per_gpu, "chunk": chunk,
+           "first_chunk": first_chunk, "steps": steps,
            "ms_per_step": el / steps * 1e3, "histories_per_sec": n_total * steps / el,
            "searched": searched, "searched_per_sec": searched * steps / el,
            "first_fail": info["first_fail"], "rounds": info["rounds"],
@@ -476,7 +478,10 @@ def main():
     ap.add_argument("--early-exit", action="store_true",
                     help="time BASELINE config 3's early-termination path instead (bank_4x16_bugs by default, "
                          "1.25M histories per GPU: 10M over 8 GPUs), sharded, QSMD_FLAG_EARLY_EXIT_BATCH")
-    ap.add_argument("--chunk", type=int, default=262144, help="--early-exit: histories per rank per round")
+    ap.add_argument("--chunk", type=int, default=262144, help="--early-exit: histories per rank per round (at most)")
+    ap.add_argument("--first-chunk", type=int, default=4096,
+                    help="--early-exit: histories per rank in the first round, x4 per round up to --chunk "
+                         "(qsmd.dist.early_chunks; 0: fixed --chunk rounds)")
     ap.add_argument("--rotate", type=int, default=5,
                     help="distinct resident batches of n-hist histories; step s checks batch s %% K, so the "
                          "library's cross-call hints come from other batches, as in a stream of new batches "
@@ -551,7 +556,7 @@ def main():
         config = args.config if args.config != "bank_4x16" else "bank_4x16_bugs"
         n_ee = args.n_hist if args.n_hist != 1_000_000 else 1_250_000
         ee = early_exit_leg(dev, rank, world, config, n_ee, args.steps, args.warmup, args.chunk, use_dist, host_group,
-                            rank == 0 and not args.no_cpu_baseline)
+                            rank == 0 and not args.no_cpu_baseline, first_chunk=args.first_chunk or None)
         if rank == 0:
             out = {"metric": "histories decided/sec, early-termination path (QSMD_FLAG_EARLY_EXIT_BATCH, sharded)",
                    "value": ee["histories_per_sec"], "unit": "histories/s", "n_gpus": world, "steps": args.steps,
@@ -559,7 +564,8 @@ def main():
                    "scaling": "weak", "vs_baseline": None, "dtype": "int32",
                    "data": "synthetic (seeded scheduler-policy generator with injected race bugs)",
                    "config": {"workload": config, "histories_per_gpu": n_ee, "parallelism": f"shard{world}",
-                              "chunk": args.chunk, "mode": "exhaustive + early exit"},
+                              "chunk": args.chunk, "first_chunk": args.first_chunk or None,
+                              "mode": "exhaustive + early exit"},
                    "early_exit": ee}
             print(json.dumps(out), file=json_out, flush=True)
         if use_dist:

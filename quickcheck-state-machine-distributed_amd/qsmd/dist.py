@@ -110,13 +110,35 @@ def chunk_slice(hdr, events, a, b):
     return h, events[lo:hi]
 
 
-def check_shard_early_exit(checker, model_id, hdr, events, n_total, rank, world, chunk=65536, group=None):
+def early_chunks(n_max, chunk, first_chunk=None, growth=4):
+    """The chunk schedule of the sharded early exit: round k checks offsets
+    [a_k, b_k) of every rank's shard (the same offsets on every rank, so each
+    rank can tell when all of them are done).  Geometric by default: the
+    first round checks ``first_chunk`` histories per rank and every round
+    ``growth`` times more, up to ``chunk`` -- a batch whose first failure
+    comes early (config 3's injected bugs: most do) is decided after a
+    small first round instead of a full chunk, while a batch without one
+    still takes only a few more rounds.  first_chunk None or >= chunk: fixed
+    chunks of ``chunk``."""
+    assert chunk > 0
+    w = chunk if not first_chunk or first_chunk >= chunk else max(1, int(first_chunk))
+    out, a = [], 0
+    while a < n_max:
+        out.append((a, min(n_max, a + w)))
+        a += w
+        w = min(chunk, w * max(1, growth))
+    return out
+
+
+def check_shard_early_exit(checker, model_id, hdr, events, n_total, rank, world, chunk=65536, group=None,
+                           first_chunk=None):
     """QSMD_FLAG_EARLY_EXIT_BATCH over a sharded batch ("a MAX
     on the early-stop flag"; here the flag carries the smallest global index
     of a failing history, a MIN all-reduce).
 
-    Each rank checks its contiguous shard in chunks of ``chunk`` histories,
-    each with the device's early exit (everything after the chunk's first
+    Each rank checks its contiguous shard in chunks (early_chunks: of
+    ``chunk`` histories, or growing from ``first_chunk`` up to it), each
+    with the device's early exit (everything after the chunk's first
     non-linearisable or raising history is SKIPPED).  After every chunk one
     MIN all-reduce publishes the global index of the first failing history
     found so far; a rank stops once its next chunk starts after it.  Every
@@ -138,18 +160,17 @@ def check_shard_early_exit(checker, model_id, hdr, events, n_total, rank, world,
     status = np.full(count, 5, dtype=np.uint8)                 # SKIPPED until searched
     nodes = np.zeros(count, dtype=np.uint64)
     starts = [shard(n_total, r, world) for r in range(world)]  # (first, count) of every rank
-    rounds_all = max((c + chunk - 1) // chunk for _, c in starts) if n_total else 0
+    sched = early_chunks(max(c for _, c in starts) if n_total else 0, chunk, first_chunk)
     best = n_total                                             # global first failure (none: n_total)
     searched = 0
     rounds = 0
-    for k in range(rounds_all):
+    for a, b in sched:
         # does any rank still have a chunk that starts before the first failure?
-        if not any(k * chunk < c and f + k * chunk < best for f, c in starts):
+        if not any(a < c and f + a < best for f, c in starts):
             break
         local = best
-        a = k * chunk
         if a < count and first + a < best:
-            b = min(count, a + chunk)
+            b = min(count, b)
             h, e = chunk_slice(hdr, events, a, b)
             st, nd = checker(model_id, h, e, early=True)
             st = np.asarray(st, dtype=np.uint8)
@@ -170,7 +191,7 @@ def check_shard_early_exit(checker, model_id, hdr, events, n_total, rank, world,
 
 
 def check_shard_early_exit_device(ctx, model_id, d_hdr, d_ev, n_events, n_total, rank, world, chunk=262144,
-                                  group=None, max_nodes=0):
+                                  group=None, max_nodes=0, first_chunk=None):
     """check_shard_early_exit on DEVICE-resident buffers (the
     reference's parallel property stops at its first failing test,
     /root/reference/test/TicketDispenser.hs:284-322).
@@ -204,8 +225,8 @@ def check_shard_early_exit_device(ctx, model_id, d_hdr, d_ev, n_events, n_total,
     status = torch.full((count,), 5, dtype=torch.uint8, device=dev)     # SKIPPED until searched
     nodes = torch.zeros(count, dtype=torch.int64, device=dev)
     starts = [shard(n_total, r, world) for r in range(world)]
-    rounds_all = max((c + chunk - 1) // chunk for _, c in starts) if n_total else 0
-    tot = torch.zeros((max(rounds_all, 1), 8), dtype=torch.int64, device=dev)
+    sched = early_chunks(max(c for _, c in starts) if n_total else 0, chunk, first_chunk)
+    tot = torch.zeros((max(len(sched), 1), 8), dtype=torch.int64, device=dev)
     local = torch.full((1,), n_total, dtype=torch.int64, device=dev)
     searched = torch.zeros((), dtype=torch.int64, device=dev)
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
@@ -217,13 +238,13 @@ def check_shard_early_exit_device(ctx, model_id, d_hdr, d_ev, n_events, n_total,
     st_ = torch.cuda.Stream(dev)
     st_.wait_stream(caller)
     with torch.cuda.stream(st_):
-        out = _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, rounds_all, chunk,
+        out = _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, sched,
                             status, nodes, tot, local, searched, multi, cdev, group, max_nodes, st_.cuda_stream)
     caller.wait_stream(st_)
     return out
 
 
-def _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, rounds_all, chunk, status,
+def _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, sched, status,
                   nodes, tot, local, searched, multi, cdev, group, max_nodes, s):
     import torch
     import torch.distributed as dist
@@ -233,12 +254,11 @@ def _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, s
     dev = d_hdr.device
     flags = device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_EARLY_EXIT_BATCH
     best, rounds = n_total, 0
-    for k in range(rounds_all):
-        if not any(k * chunk < c and f + k * chunk < best for f, c in starts):
+    for k, (a, b) in enumerate(sched):
+        if not any(a < c and f + a < best for f, c in starts):
             break
-        a = k * chunk
         if a < count and first + a < best:
-            b = min(count, a + chunk)
+            b = min(count, b)
             ctx.check_device(model_id, d_hdr.data_ptr() + 16 * a, b - a, d_ev.data_ptr(), n_events,
                              status.data_ptr() + a, nodes.data_ptr() + 8 * a, None, tot[k].data_ptr(),
                              flags=flags, max_nodes=max_nodes, stream=s)

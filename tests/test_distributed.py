@@ -127,7 +127,7 @@ def planted_stream(config, n_total, plant):
     return hdr, ev
 
 
-def _early_worker(rank, world, port, config, n_total, plant, chunk, out_q):
+def _early_worker(rank, world, port, config, n_total, plant, chunk, first_chunk, out_q):
     sys.path[:0] = [os.path.join(HERE, "..", "quickcheck-state-machine-distributed_amd"),
                     os.path.join(HERE, "..", "oracle"), HERE]
     import torch.distributed as dist
@@ -143,16 +143,20 @@ def _early_worker(rank, world, port, config, n_total, plant, chunk, out_q):
         first, count = qdist.shard(n_total, rank, world)
         h, e = qdist.chunk_slice(hdr, ev, first, first + count)
         st, nd, info = qdist.check_shard_early_exit(_oracle_early_checker, gen.CONFIGS[config]["model_id"], h, e,
-                                                    n_total, rank, world, chunk=chunk)
+                                                    n_total, rank, world, chunk=chunk, first_chunk=first_chunk)
         tot, _ = qdist.allreduce_totals(qdist.totals_from_status(st, nd))
         out_q.put((rank, st.tolist(), [int(x) for x in nd], info, tot.tolist()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("config,plant,chunk", [("bank_4x16_bugs", None, 200), ("bank_4x16", 2300, 256),
-                                                ("bank_4x16", 700, 128), ("bank_4x16", None, 500)])
-def test_two_rank_gloo_early_exit(config, plant, chunk):
+@pytest.mark.parametrize("config,plant,chunk,first_chunk", [
+    ("bank_4x16_bugs", None, 200, None), ("bank_4x16", 2300, 256, None), ("bank_4x16", 700, 128, None),
+    ("bank_4x16", None, 500, None),
+    # the geometric schedule (early_chunks: 16, 64, 256, ... per rank)
+    ("bank_4x16_bugs", None, 256, 16), ("bank_4x16", 2300, 256, 16), ("bank_4x16", 700, 500, 16),
+    ("bank_4x16", None, 500, 16)])
+def test_two_rank_gloo_early_exit(config, plant, chunk, first_chunk):
     from qsmd import dist as qdist
     from qsmd import gen
 
@@ -160,7 +164,7 @@ def test_two_rank_gloo_early_exit(config, plant, chunk):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_early_worker, args=(r, world, port, config, n_total, plant, chunk, q))
+    procs = [ctx.Process(target=_early_worker, args=(r, world, port, config, n_total, plant, chunk, first_chunk, q))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -183,7 +187,10 @@ def test_two_rank_gloo_early_exit(config, plant, chunk):
     if first_fail < n_total:
         assert first_fail + 1 <= searched < n_total  # everything up to the failure, and less than all
         if first_fail < 1500:                        # in rank 0's shard: rank 1 stops once it is known
-            assert results[1][2]["searched"] <= (first_fail // chunk + 1) * chunk
+            sched = qdist.early_chunks(1501, chunk, first_chunk)
+            k = next(i for i, (a, b) in enumerate(sched) if a <= first_fail < b)
+            assert results[1][2]["searched"] <= sched[k][1]
+            assert results[0][2]["rounds"] == k + 1
     else:
         assert searched == n_total
 
@@ -296,3 +303,15 @@ def test_round_windows():
             w = qdist.round_windows(n, world)
             assert (w[0][0] if w else 0) == 0 and (w[-1][1] if w else n) == n
             assert all(a[1] == b[0] for a, b in zip(w, w[1:]))
+
+
+def test_early_chunks_schedule():
+    from qsmd import dist as qdist
+    assert qdist.early_chunks(10, 4) == [(0, 4), (4, 8), (8, 10)]
+    assert qdist.early_chunks(10, 4, first_chunk=8) == [(0, 4), (4, 8), (8, 10)]
+    assert qdist.early_chunks(100, 32, first_chunk=2) == [(0, 2), (2, 10), (10, 42), (42, 74), (74, 100)]
+    assert qdist.early_chunks(0, 32, first_chunk=2) == []
+    for n, c, f in [(3001, 256, 16), (1 << 20, 262144, 4096), (7, 1, 1)]:
+        s = qdist.early_chunks(n, c, f)
+        assert s[0][0] == 0 and s[-1][1] == n and all(b0 == a1 for (_, b0), (a1, _) in zip(s, s[1:]))
+        assert all(0 < b - a <= c for a, b in s)

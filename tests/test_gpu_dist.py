@@ -94,12 +94,13 @@ def _worker(rank, world, port, n_total, out_q):
             first, count = qdist.shard(n_total, rank, world)
             h, e = qdist.chunk_slice(hdr, ev, first, first + count)
             st, nd, info = qdist.check_shard_early_exit(qdist.device_checker(ctx, max_nodes=10**7), mid, h, e,
-                                                        n_total, rank, world, chunk=2048)
+                                                        n_total, rank, world, chunk=2048,
+                                                        first_chunk=128)
             # the same on device-resident buffers (one MIN all-reduce per chunk, statuses stay on the GPU)
             d_h = torch.from_numpy(h.view(np.uint8)).cuda()
             d_e = torch.from_numpy(e.view(np.uint8)).cuda()
             dst, dnd, dinfo = qdist.check_shard_early_exit_device(ctx, mid, d_h, d_e, len(e), n_total, rank, world,
-                                                                  chunk=2048, max_nodes=10**7)
+                                                                  chunk=2048, max_nodes=10**7, first_chunk=128)
             dtot, _ = qdist.allreduce_totals(dinfo.pop("totals"))
             dev_res = (dst.cpu().tolist(), dnd.cpu().tolist(), dinfo, dtot.tolist())
             one = None
