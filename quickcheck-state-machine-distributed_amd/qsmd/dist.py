@@ -198,18 +198,20 @@ def check_shard_early_exit_device(ctx, model_id, d_hdr, d_ev, n_events, n_total,
 
     d_hdr / d_ev: this rank's shard as uint8 torch tensors on its GPU (the
     include/qsmd.h records; ev_off relative to d_ev).  Each round checks the
-    rank's next chunk in place through qsmd_check_batch_device with
-    QSMD_FLAG_EARLY_EXIT_BATCH (headers at the chunk's offset, the shard's
-    whole event buffer, outputs into the shard's status / node arrays).  The
-    chunk's first failure comes from its device totals -- with the flag every
-    history after it is SKIPPED, so it is the chunk's last history minus the
-    skipped count -- and one MIN all-reduce per round (RCCL on a device
-    tensor under nccl) publishes the global first failure; its 8-byte result
-    is the only value that reaches the host per round, for the decision to
-    stop.  Status and node arrays stay on the device.  The calls and the torch
-    ops run on a stream of their own, ordered after the caller's.  Same rounds, stopping
-    rule and final SKIPPED marking as the host version, so status, nodes and
-    totals equal one context's early exit over the concatenated batch.
+    rank's next chunk (early_chunks) in place through qsmd_check_batch_device
+    with QSMD_FLAG_EARLY_EXIT_BATCH (headers at the chunk's offset, the
+    shard's whole event buffer, outputs into the shard's status / node
+    arrays).  The chunk's first failure comes from its device totals -- with
+    the flag every history after it is SKIPPED, so it is the chunk's last
+    history minus the skipped count; the 64-byte totals row is the only
+    thing read back per round, and one MIN all-reduce per round (RCCL on a
+    device tensor under nccl) publishes the global first failure.  Status
+    and node arrays stay on the device; the totals are the rounds' rows
+    (summed on the host) less the histories searched after the global first
+    failure, which end SKIPPED.  The calls and copies run on a stream of
+    their own, ordered after the caller's.  Same rounds, stopping rule and
+    final SKIPPED marking as the host version, so status, nodes and totals
+    equal one context's early exit over the concatenated batch.
 
     Returns (status u8 tensor, nodes i64 tensor, info) for this rank's shard;
     info: first_fail (n_total if none), rounds, searched (histories the
@@ -218,34 +220,41 @@ def check_shard_early_exit_device(ctx, model_id, d_hdr, d_ev, n_events, n_total,
     import torch
     import torch.distributed as dist
 
-    from . import device
-
     first, count = shard(n_total, rank, world)
     dev = d_hdr.device
-    status = torch.full((count,), 5, dtype=torch.uint8, device=dev)     # SKIPPED until searched
-    nodes = torch.zeros(count, dtype=torch.int64, device=dev)
     starts = [shard(n_total, r, world) for r in range(world)]
     sched = early_chunks(max(c for _, c in starts) if n_total else 0, chunk, first_chunk)
-    tot = torch.zeros((max(len(sched), 1), 8), dtype=torch.int64, device=dev)
-    local = torch.full((1,), n_total, dtype=torch.int64, device=dev)
-    searched = torch.zeros((), dtype=torch.int64, device=dev)
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
     cdev = _collective_device(group) if multi else dev
     # the calls and the torch ops below on one stream of their own (torch's
     # default stream is handle 0, which the C ABI reads as "the context's
     # stream": nothing would order the two), joined to the caller's at the end
     caller = torch.cuda.current_stream(dev)
-    st_ = torch.cuda.Stream(dev)
+    st_ = _side_stream(dev)
     st_.wait_stream(caller)
     with torch.cuda.stream(st_):
-        out = _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, sched,
-                            status, nodes, tot, local, searched, multi, cdev, group, max_nodes, st_.cuda_stream)
+        out = _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, sched, multi, cdev,
+                            group, max_nodes, st_.cuda_stream)
     caller.wait_stream(st_)
     return out
 
 
-def _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, sched, status,
-                  nodes, tot, local, searched, multi, cdev, group, max_nodes, s):
+_SIDE_STREAMS = {}
+
+
+def _side_stream(dev):
+    """One side stream per device for the early-exit rounds (creating a HIP
+    stream per call cost more than the rounds themselves)."""
+    import torch
+
+    k = dev.index if dev.index is not None else torch.cuda.current_device()
+    if k not in _SIDE_STREAMS:
+        _SIDE_STREAMS[k] = torch.cuda.Stream(dev)
+    return _SIDE_STREAMS[k]
+
+
+def _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, sched, multi, cdev, group,
+                  max_nodes, s):
     import torch
     import torch.distributed as dist
 
@@ -253,36 +262,53 @@ def _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, s
 
     dev = d_hdr.device
     flags = device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_EARLY_EXIT_BATCH
-    best, rounds = n_total, 0
+    status = torch.empty(count, dtype=torch.uint8, device=dev)   # written by the calls, the rest filled below
+    nodes = torch.empty(count, dtype=torch.int64, device=dev)
+    tot = torch.empty((max(len(sched), 1), 8), dtype=torch.int64, device=dev)
+    acc = np.zeros(8, dtype=np.int64)                          # the rounds' totals rows
+    best, rounds, searched, end = n_total, 0, 0, 0             # [0, end): the histories this rank checked
     for k, (a, b) in enumerate(sched):
         if not any(a < c and f + a < best for f, c in starts):
             break
+        local = best
         if a < count and first + a < best:
             b = min(count, b)
             ctx.check_device(model_id, d_hdr.data_ptr() + 16 * a, b - a, d_ev.data_ptr(), n_events,
                              status.data_ptr() + a, nodes.data_ptr() + 8 * a, None, tot[k].data_ptr(),
                              flags=flags, max_nodes=max_nodes, stream=s)
-            t = tot[k]
-            ff = (first + b - 1) - t[6]                        # the chunk's first failure, if it has one
-            local = torch.where((t[2] + t[3]) > 0, torch.minimum(local, ff), local)
-            searched += (b - a) - t[6]
-        r = local.to(cdev)
+            t = tot[k].cpu().numpy()                           # (waits for the call: s is the current stream)
+            acc += t
+            end = b
+            searched += (b - a) - int(t[6])
+            if t[2] + t[3] > 0:                                # the chunk's first failure
+                local = min(local, first + b - 1 - int(t[6]))
         if multi:
+            r = torch.full((1,), local, dtype=torch.int64, device=cdev)
             dist.all_reduce(r, op=dist.ReduceOp.MIN, group=group)
-        best = int(r.item())
-        local.fill_(best)
+            best = int(r.item())
+        else:
+            best = local
         rounds += 1
     cut = best - first                                         # local index of the global first failure
-    if cut < count:
-        after = max(0, cut + 1)
-        status[after:] = 5
-        nodes[after:] = 0
-    t = torch.zeros(8, dtype=torch.int64, device=dev)
-    bc = torch.bincount(status.to(torch.int64), minlength=6)
-    t[1], t[2], t[3], t[4], t[5], t[6] = bc[1], bc[0], bc[2], bc[3], bc[4], bc[5]
-    t[0] = bc[0] + bc[1] + bc[2]
-    t[7] = nodes.sum()
-    return status, nodes, dict(first_fail=best, rounds=rounds, searched=int(searched.item()), totals=t)
+    after = max(0, cut + 1) if cut < count else count          # [after, count) ends SKIPPED with 0 nodes
+    if after < end:                                            # searched after it: out of the totals
+        seg = status[after:end]
+        codes = torch.arange(6, dtype=torch.uint8, device=dev)
+        v = torch.cat([(seg.unsqueeze(1) == codes).sum(0), nodes[after:end].sum().view(1)]).cpu().numpy()
+        acc -= totals_from_counts(v[:6], int(v[6]))
+    lo = min(after, end)
+    if lo < count:
+        status[lo:] = 5
+        nodes[lo:] = 0
+    acc[6] += count - after
+    t = torch.from_numpy(acc).to(dev, non_blocking=False)
+    return status, nodes, dict(first_fail=best, rounds=rounds, searched=searched, totals=t)
+
+
+def totals_from_counts(counts, nodes):
+    """qsmd_totals from the count of each status (0..5) and a node sum."""
+    c = [int(x) for x in counts]
+    return np.array([c[0] + c[1] + c[2], c[1], c[0], c[2], c[3], c[4], c[5], int(nodes)], dtype=np.int64)
 
 
 def device_checker(ctx, max_nodes=0):
