@@ -890,18 +890,12 @@ __device__ __forceinline__ void beat(const SplitArgs& p, int lane, uint32_t k, u
         __hip_atomic_store(p.debug + (uint64_t)blockIdx.x * 4 + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The giant stage's work (a call with giants or the early exit): out of
-// line, so that a call without giants -- nearly every call -- runs the
-// kernel's short path alone (the functions below take the arguments by
-// reference; from the kernel's own parameter that made a private copy of
-// them, ~400 B per lane, at every launch)
+// The frontier, task and combine phases (n_g > 0 giants).
 template <uint32_t MODEL>
-__device__ __noinline__ void giant_work(const SplitArgs& p, uint32_t n_g, GiantLds<MODEL>& u) {
+__device__ __forceinline__ void giant_phases(const SplitArgs& p, uint32_t n_g, GiantLds<MODEL>& u, uint64_t t0) {
     const SearchArgs& a = p.s;
     const int lane = threadIdx.x;
     uint32_t* cnt = p.cnt;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    beat(p, lane, 0, 1);
     // ---- frontier: chunks of 64 giants; variant 0 on all lanes, then variant
     // 1 in four rounds of 16 lanes
     for (;;) {
@@ -964,27 +958,53 @@ __device__ __noinline__ void giant_work(const SplitArgs& p, uint32_t n_g, GiantL
         publish_add(cnt + C_CDONE, min(64u, n_g - c0), lane);
     }
     cc.flush(a.buckets, lane);
+}
+
+// The giant stage's work (a call with giants or the early exit): out of
+// line, so that a call without giants -- nearly every call -- runs the
+// kernel's short path alone (the functions below take the arguments by
+// reference; from the kernel's own parameter that made a private copy of
+// them, ~400 B per lane, at every launch)
+template <uint32_t MODEL>
+__device__ __noinline__ void giant_work(const SplitArgs& p, uint32_t n_g, GiantLds<MODEL>& u) {
+    const SearchArgs& a = p.s;
+    const int lane = threadIdx.x;
+    uint32_t* cnt = p.cnt;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    beat(p, lane, 0, 1);
+    // (no giant: an early-exit call goes straight to the fixup -- the giant
+    // count is final here, every stage that appends ran before this launch,
+    // and without a frontier there are no tasks; the phases' queue and
+    // done-counter atomics in every workgroup cost ~60 us per call)
+    if (n_g) giant_phases<MODEL>(p, n_g, u, t0);
     // ---- early exit: every history after the first failing one is SKIPPED,
     // and the totals are recounted from the final outputs
     if (p.early) {
-        (void)wait_for(cnt + C_CDONE, n_g, a, t0);
+        if (n_g) (void)wait_for(cnt + C_CDONE, n_g, a, t0);
         const uint32_t ff = ld_cnt(a.first_fail);
         Counters xc;
         uint64_t skipped = 0;
         constexpr uint32_t kChunk = 4096;
+        uint8_t* const st_out = a.status;
+        uint64_t* const nd_out = a.nodes;
+        const uint64_t n_hist = a.n_hist;
         for (;;) {
             uint32_t c0 = 0;
             if (lane == 0) c0 = atomicAdd(cnt + C_XNEXT, 1u);
             const uint64_t b0 = (uint64_t)__shfl(c0, 0, 64) * kChunk;
-            if (b0 >= a.n_hist) break;
-            for (uint64_t hh = b0 + (uint64_t)lane; hh < a.n_hist && hh < b0 + kChunk; hh += 64) {
-                if (hh > ff) {
-                    a.status[hh] = QSMD_STATUS_SKIPPED;
-                    if (a.nodes) a.nodes[hh] = 0;
-                    ++skipped;
-                } else {
-                    xc.add(a.status[hh], a.nodes ? a.nodes[hh] : 0ull);
-                }
+            if (b0 >= n_hist) break;
+            // the histories up to the first failure counted (loads only),
+            // then the rest marked (stores only), the pointers and bounds
+            // in registers: a byte store may alias the argument block the
+            // loop read them from, and vmcnt counts stores too, so each
+            // reload waited for the row's stores (a 4096-history chunk ~33 us)
+            const uint64_t e0 = min(n_hist, b0 + kChunk);
+            const uint64_t keep = min(e0, (uint64_t)ff + 1u);
+            for (uint64_t hh = b0 + (uint64_t)lane; hh < keep; hh += 64) xc.add(st_out[hh], nd_out ? nd_out[hh] : 0ull);
+            for (uint64_t hh = max(b0, keep) + (uint64_t)lane; hh < e0; hh += 64) {
+                st_out[hh] = QSMD_STATUS_SKIPPED;
+                if (nd_out) nd_out[hh] = 0;
+                ++skipped;
             }
         }
         xc.flush(a.buckets + (size_t)kBuckets * kBucketWords, lane);

@@ -207,16 +207,17 @@ def check_shard_early_exit_device(ctx, model_id, d_hdr, d_ev, n_events, n_total,
     thing read back per round, and one MIN all-reduce per round (RCCL on a
     device tensor under nccl) publishes the global first failure.  Status
     and node arrays stay on the device; the totals are the rounds' rows
-    (summed on the host) less the histories searched after the global first
-    failure, which end SKIPPED.  The calls and copies run on a stream of
-    their own, ordered after the caller's.  Same rounds, stopping rule and
+    summed on the host, with every history after the global first failure
+    SKIPPED (no status is read back for that: see _early_rounds).  The
+    calls and copies run on a stream of their own, ordered after the
+    caller's.  Same rounds, stopping rule and
     final SKIPPED marking as the host version, so status, nodes and totals
     equal one context's early exit over the concatenated batch.
 
     Returns (status u8 tensor, nodes i64 tensor, info) for this rank's shard;
     info: first_fail (n_total if none), rounds, searched (histories the
-    device did not skip), totals (this rank's, int64[8] tensor on the
-    device) -- all-reduce them with allreduce_totals for the batch's."""
+    device did not skip), totals (this rank's, an int64[8] host tensor) --
+    all-reduce them with allreduce_totals for the batch's."""
     import torch
     import torch.distributed as dist
 
@@ -289,26 +290,20 @@ def _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, s
         else:
             best = local
         rounds += 1
-    cut = best - first                                         # local index of the global first failure
-    after = max(0, cut + 1) if cut < count else count          # [after, count) ends SKIPPED with 0 nodes
-    if after < end:                                            # searched after it: out of the totals
-        seg = status[after:end]
-        codes = torch.arange(6, dtype=torch.uint8, device=dev)
-        v = torch.cat([(seg.unsqueeze(1) == codes).sum(0), nodes[after:end].sum().view(1)]).cpu().numpy()
-        acc -= totals_from_counts(v[:6], int(v[6]))
-    lo = min(after, end)
+    # The statuses after the global first failure end SKIPPED with 0 nodes.
+    # Before this rank's shard (cut < 0): all of it.  In it: the failure is
+    # this rank's own, found in the last chunk it checked (a rank stops at
+    # its first), whose early exit already SKIPPED the rest of that chunk --
+    # so the rows hold, and only the chunks never checked are left.
+    cut = best - first
+    lo = 0 if cut < 0 else end
+    if cut < 0:
+        acc[:] = 0
+    acc[6] += count - lo
     if lo < count:
         status[lo:] = 5
         nodes[lo:] = 0
-    acc[6] += count - after
-    t = torch.from_numpy(acc).to(dev, non_blocking=False)
-    return status, nodes, dict(first_fail=best, rounds=rounds, searched=searched, totals=t)
-
-
-def totals_from_counts(counts, nodes):
-    """qsmd_totals from the count of each status (0..5) and a node sum."""
-    c = [int(x) for x in counts]
-    return np.array([c[0] + c[1] + c[2], c[1], c[0], c[2], c[3], c[4], c[5], int(nodes)], dtype=np.int64)
+    return status, nodes, dict(first_fail=best, rounds=rounds, searched=searched, totals=torch.from_numpy(acc))
 
 
 def device_checker(ctx, max_nodes=0):
