@@ -880,12 +880,13 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     }
     {
         // (2 per CU when the last call had giants; an early exit without
-        // them: one workgroup per fixup chunk of 4096 histories, at least 8
-        // -- every workgroup of the launch takes the fixup's queue and exit
-        // atomics, 2 per CU made a 4096-history call's giant stage ~65 us)
+        // them: one workgroup per fixup chunk, at least 8 and at most 2 per
+        // CU -- every workgroup of the launch takes the fixup's queue and
+        // exit atomics, 2 per CU made a 4096-history call's giant stage ~65 us)
         const uint64_t gg = c->giant_grid ? c->giant_grid
                           : (hint[3] ? 2ull * c->n_cu
-                                     : (early ? std::min<uint64_t>(2ull * c->n_cu, std::max<uint64_t>(8, (n_hist + 4095) / 4096))
+                                     : (early ? std::min<uint64_t>(2ull * c->n_cu,
+                                                                   std::max<uint64_t>(8, (n_hist + kFixupChunk - 1) / kFixupChunk))
                                               : 64ull));
         if (sync_stages()) p.debug = giant_debug_buffer(c, gg);
         HIP_TRY(c, launch_giants(p, (uint32_t)gg, s), "giant launch");

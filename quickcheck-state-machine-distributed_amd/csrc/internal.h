@@ -173,6 +173,12 @@ constexpr int kProbeBudget = 6;   // the call's stage-0 budget and batch size (a
 constexpr int kProbeN = 7;
 constexpr int kProbeWritten = 8;  // 1 once a call's giant stage wrote the probe (never reset)
 
+// Histories per early-exit fixup chunk of the giant stage (a workgroup takes
+// one at a time; a wavefront marks ~0.33 us per row of 64, so short chunks
+// spread a small batch's fixup over more workgroups; api.hip sizes the grid
+// by them)
+constexpr uint32_t kFixupChunk = 512;
+
 // internal status: the search was handed to a later stage (not a result)
 constexpr int QSMD_STATUS_HANDED_OFF = 0x40;
 

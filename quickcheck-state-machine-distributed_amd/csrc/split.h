@@ -984,7 +984,7 @@ __device__ __noinline__ void giant_work(const SplitArgs& p, uint32_t n_g, GiantL
         const uint32_t ff = ld_cnt(a.first_fail);
         Counters xc;
         uint64_t skipped = 0;
-        constexpr uint32_t kChunk = 4096;
+        constexpr uint32_t kChunk = kFixupChunk;
         uint8_t* const st_out = a.status;
         uint64_t* const nd_out = a.nodes;
         const uint64_t n_hist = a.n_hist;
