@@ -533,6 +533,34 @@ def test_early_exit_batch(ctx, knobs, name, shift):
     assert tot["checked"] == int(((st_o[:cut + 1] <= 2)).sum())
 
 
+def test_early_exit_fixup_chunks(ctx, knobs):
+    """The early-exit fixup runs in 512-history chunks, one workgroup each
+    (a grid sized by them when the last call had no giants, 2 per CU when it
+    had): a failure planted before, at and after chunk boundaries, at the
+    batch's ends, and none, in a row of calls whose giant hint flips (a
+    split knob that makes giants of the heavy histories, then none).
+    Everything up to the failure is the oracle's, everything after it
+    SKIPPED with 0 nodes, and the totals count exactly that."""
+    from test_distributed import planted_stream
+    from qsmd import device
+    n = 5000
+    for plant, split in [(None, 0), (511, 0), (512, 0), (513, 0), (0, 0), (n - 1, 0), (1023, 2), (4100, 2),
+                         (2047, 0), (None, 2), (3000, 0)]:
+        hdr, ev = planted_stream("bank_4x16", n, plant)
+        st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr, ev, threads=8, max_nodes=10**7)
+        fails = np.nonzero((st_o == 0) | (st_o == 2))[0]
+        cut = int(fails[0]) if len(fails) else n
+        knobs(split_budget=split if split else 1024, stage0_budget=8)
+        st, nd, _, tot = ctx.check_arrays(models.MODEL_BANK, hdr, ev, max_nodes=10**7,
+                                          flags=device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_EARLY_EXIT_BATCH)
+        assert np.array_equal(st[:cut + 1], st_o[:cut + 1]), plant
+        assert np.array_equal(nd[:cut + 1], nd_o[:cut + 1]), plant
+        assert (st[cut + 1:] == codec.STATUS_SKIPPED).all() and (nd[cut + 1:] == 0).all(), plant
+        assert tot["skipped"] == max(0, n - cut - 1), plant
+        assert tot["nodes"] == int(nd_o[:cut + 1].sum()), plant
+        assert tot["checked"] == int((st_o[:cut + 1] <= 2).sum()), plant
+
+
 def test_encode_errors(ctx):
     hdr = np.zeros(5, dtype=codec.HDR_DTYPE)
     ev = np.zeros(8, dtype=codec.EV_DTYPE)
