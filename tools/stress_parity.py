@@ -28,7 +28,8 @@ KNOBS = {"stage0_budget": [0, 4, 16, 32, 40, 64], "stage0w_budget": [0, 4, 32], 
          "split_budget": [1, 16, 64, 1024], "memo_lane_entries": [2, 256], "wave_grid": [0, 5],
          "wave_min_rem": [0, 4, 64], "split_xmemo": [0, 1], "memo_lds": [0, 1, 2], "dag_states": [0, 6, 128, 1024],
          "stage0_budget_auto": [0, 1], "memo_after": [1, 32, 100], "timing_events": [0, 1],
-         "fold": [0, 1], "resume_cap": [0, 1, 7, 64]}
+         "fold": [0, 1], "resume_cap": [0, 1, 7, 64],
+         "early": [0, 0, 0, 1]}   # (early: QSMD_FLAG_EARLY_EXIT_BATCH for the batch, not a context knob)
 DEFAULT_KNOBS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 2, "split_budget": 1024,
                  "memo_lane_entries": 128, "wave_grid": 0, "wave_min_rem": 4, "split_xmemo": 1,
                  "memo_lds": 1, "dag_states": 128, "stage0_budget_auto": 1, "memo_after": 32, "timing_events": 0,
@@ -43,8 +44,16 @@ def run(ctx, batches=40, seed=1, knobs=False, wide=False, only=-1, dump=None, lo
     t0 = time.time()
 
     def compare(model_id, hdr, ev, batch, kn):
-        st_d, nd_d, w_d, _ = ctx.check_arrays(model_id, hdr, ev, None, max_nodes=200_000, witness=True)
+        early = bool(kn.get("early"))
+        flags = device.QSMD_FLAG_EXHAUSTIVE | (device.QSMD_FLAG_EARLY_EXIT_BATCH if early else 0)
+        st_d, nd_d, w_d, _ = ctx.check_arrays(model_id, hdr, ev, None, max_nodes=200_000, witness=True, flags=flags)
         st_o, nd_o, w_o = oracle_c.check_batch(model_id, hdr, ev, None, 200_000, 16, witness=True)
+        if early:                                    # everything after the first failure: SKIPPED, 0 nodes
+            fails = np.nonzero((st_o == 0) | (st_o == 2))[0]
+            if len(fails):
+                st_o, nd_o = st_o.copy(), nd_o.copy()
+                st_o[fails[0] + 1:] = codec.STATUS_SKIPPED
+                nd_o[fails[0] + 1:] = 0
         # the safety net fired: its BUDGET results are not the reference's, but
         # every other result of the batch still must be (recorded and compared)
         cmp = np.ones(len(hdr), dtype=bool)
@@ -80,7 +89,8 @@ def run(ctx, batches=40, seed=1, knobs=False, wide=False, only=-1, dump=None, lo
             if knobs:
                 for k, vals in KNOBS.items():
                     kn[k] = rng.choice(vals)
-                    ctx.set_param(k, kn[k])
+                    if k != "early":
+                        ctx.set_param(k, kn[k])
             check = only < 0 or only == b
             if b % 2 == 0:                               # generator with random parameters
                 name = rng.choice(list(gen.CONFIGS))
@@ -120,7 +130,8 @@ def run(ctx, batches=40, seed=1, knobs=False, wide=False, only=-1, dump=None, lo
     finally:
         if knobs:
             for k, v in DEFAULT_KNOBS.items():
-                ctx.set_param(k, v)
+                if k != "early":
+                    ctx.set_param(k, v)
     stats["seconds"] = round(time.time() - t0, 1)
     return stats
 
