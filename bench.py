@@ -19,6 +19,8 @@ loads another build of libqsmd.so.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+    python bench.py --early-exit      (BASELINE config 3's early-termination
+                                       path: histories decided per second)
 
 Rank 0 prints one JSON line.  At N = 1 it also reports (outside the timed
 region of `value`): the CPU baselines on the host's cores -- the C oracle
