@@ -222,11 +222,7 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
             if constexpr (LT) {
                 if (k.ok) hit = memo_lookup_lds<MODEL, G>(tab, k, h, cnt);
             } else {
-#ifndef QSMD_NO_WRITTEN_MAP
                 if (k.ok && wr.maybe(k.slot)) hit = memo_lookup<MODEL, G>(tab, k, h, cnt);
-#else
-                if (k.ok) hit = memo_lookup<MODEL, G>(tab, k, h, cnt);
-#endif
             }
             if (hit) {
                 if (d.nodes + cnt > limit) {      // the budget falls inside that subtree
