@@ -227,3 +227,50 @@ def test_bench_two_ranks_on_one_gpu():
     assert d["n_gpus"] == 2 and d["steps"] == 6 and d["value"] > 0
     assert d["verdicts"]["checked"] + d["verdicts"]["budget"] <= 2 * 6 * 20000
     assert "gloo" in d["config"]["counters"] and d["config"]["exchange_ms"] is not None
+
+
+@pytest.mark.parametrize("n_total,plant,chunk,first_chunk", [
+    (0, None, 4096, 64), (1, None, 4096, 64), (1, 0, 4096, 64), (5, 4, 2, 1), (3000, None, 1000, 4096),
+    (3000, 2999, 512, 16), (3000, 0, 512, 16), (3000, 1500, 700, 100)])
+def test_device_early_exit_one_rank(n_total, plant, chunk, first_chunk):
+    """check_shard_early_exit_device without a process group (one rank): an
+    empty batch, one history, a failure at either end or in the middle, no
+    failure, a first chunk larger than the chunk; the statuses, counts and
+    totals of one context's early exit over the batch, the rounds of the
+    schedule up to the failure's chunk."""
+    _paths()
+    import torch
+
+    import oracle_c
+    from test_distributed import early_exit_reference, planted_stream
+    from qsmd import device, gen
+    from qsmd import dist as qdist
+
+    config = "bank_4x16"
+    mid = gen.CONFIGS[config]["model_id"]
+    hdr, ev = planted_stream(config, max(n_total, 1), plant)
+    if n_total == 0:
+        hdr, ev = hdr[:0], ev[:0]
+    ctx = device.Context(0)
+    try:
+        d_h = torch.from_numpy(np.ascontiguousarray(hdr).view(np.uint8)).cuda()
+        d_e = torch.from_numpy(np.ascontiguousarray(ev).view(np.uint8)).cuda()
+        st, nd, info = qdist.check_shard_early_exit_device(ctx, mid, d_h, d_e, len(ev), n_total, 0, 1, chunk=chunk,
+                                                           max_nodes=10**7, first_chunk=first_chunk)
+        torch.cuda.synchronize()
+        st, nd = st.cpu().numpy(), nd.cpu().numpy().astype(np.uint64)
+    finally:
+        ctx.close()
+    if n_total:
+        st_full, nd_full, _ = oracle_c.check_batch(mid, hdr, ev, threads=4, max_nodes=10**7)
+    else:
+        st_full, nd_full = np.zeros(0, dtype=np.uint8), np.zeros(0, dtype=np.uint64)
+    st_ref, nd_ref = early_exit_reference(np.asarray(st_full), np.asarray(nd_full))
+    assert np.array_equal(st, st_ref) and np.array_equal(nd, nd_ref)
+    assert info["totals"].tolist() == qdist.totals_from_status(st_ref, nd_ref).tolist()
+    fails = np.nonzero((np.asarray(st_full) == 0) | (np.asarray(st_full) == 2))[0]
+    ff = int(fails[0]) if len(fails) else n_total
+    assert info["first_fail"] == ff
+    sched = qdist.early_chunks(n_total, chunk, first_chunk)
+    assert info["rounds"] == (next(i for i, (a, b) in enumerate(sched) if a <= ff < b) + 1 if ff < n_total
+                              else len(sched))
