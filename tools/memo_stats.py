@@ -69,7 +69,8 @@ def main():
         "group_start_us_max": round(float(start.max()), 1),
         "staging_us_median": round(float(np.median(staged)), 2),
         "group_span_us": {"median": round(float(np.median(span)), 1), "max": round(float(span.max()), 1)},
-        "max_iterations": {"median": int(np.median(q[:, 3])), "max": int(q[:, 3].max())},
+        "max_iterations": {"median": int(np.median(q[:, 3])), "p90": int(np.percentile(q[:, 3], 90)),
+                           "p99": int(np.percentile(q[:, 3], 99)), "max": int(q[:, 3].max())},
         "iterations_total": int(q[:, 4].sum()),
         "lane_utilisation": round(float(q[:, 4].sum()) / float((q[:, 3] * 64).sum()), 3),
         "iterations_per_history": {"mean": round(float(q[:, 4].sum()) / float(q[:, 6].sum()), 1)},
