@@ -230,12 +230,17 @@ def check_shard_early_exit_device(ctx, model_id, d_hdr, d_ev, n_events, n_total,
     # the calls and the torch ops below on one stream of their own (torch's
     # default stream is handle 0, which the C ABI reads as "the context's
     # stream": nothing would order the two), joined to the caller's at the end
+    # (the outputs allocated on the caller's stream, which waits for the side
+    # stream before it returns: the caching allocator never sees them freed
+    # while the side stream still writes them)
+    status = torch.empty(count, dtype=torch.uint8, device=dev)   # written by the calls, the rest filled
+    nodes = torch.empty(count, dtype=torch.int64, device=dev)
     caller = torch.cuda.current_stream(dev)
     st_ = _side_stream(dev)
     st_.wait_stream(caller)
     with torch.cuda.stream(st_):
         out = _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, sched, multi, cdev,
-                            group, max_nodes, st_.cuda_stream)
+                            group, max_nodes, st_.cuda_stream, status, nodes)
     caller.wait_stream(st_)
     return out
 
@@ -255,7 +260,7 @@ def _side_stream(dev):
 
 
 def _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, starts, sched, multi, cdev, group,
-                  max_nodes, s):
+                  max_nodes, s, status, nodes):
     import torch
     import torch.distributed as dist
 
@@ -263,8 +268,6 @@ def _early_rounds(ctx, model_id, d_hdr, d_ev, n_events, n_total, first, count, s
 
     dev = d_hdr.device
     flags = device.QSMD_FLAG_EXHAUSTIVE | device.QSMD_FLAG_EARLY_EXIT_BATCH
-    status = torch.empty(count, dtype=torch.uint8, device=dev)   # written by the calls, the rest filled below
-    nodes = torch.empty(count, dtype=torch.int64, device=dev)
     tot = torch.empty((max(len(sched), 1), 8), dtype=torch.int64, device=dev)
     acc = np.zeros(8, dtype=np.int64)                          # the rounds' totals rows
     best, rounds, searched, end = n_total, 0, 0, 0             # [0, end): the histories this rank checked
