@@ -20,7 +20,11 @@ loads another build of libqsmd.so.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
     python bench.py --early-exit      (BASELINE config 3's early-termination
-                                       path: histories decided per second)
+                                       path: ms to the decision, histories
+                                       searched per second up to it)
+    python bench.py --early-exit --plant 0.6   (config 2's stream with one
+                                       failure planted at 60 % of the batch:
+                                       the geometric rounds and a MIN per round)
 
 Rank 0 prints one JSON line.  At N = 1 it also reports (outside the timed
 region of `value`): the CPU baselines on the host's cores -- the C oracle
@@ -142,6 +146,7 @@ class InFlight:
         self.last = (0, 0)
         self.totals = None
         self.exchange_ms = None
+        self.elapsed_incl_exchange = None
 
     def step(self):
         k = self.steps_run
@@ -241,12 +246,15 @@ class InFlight:
         for c in self.ctxs:
             c.set_param("timing_events", 1)
         torch.cuda.synchronize(self.dev)
+        # the window plus the exchange that follows it: the whole job's time
+        # with its only collective (value_incl_exchange)
+        self.elapsed_incl_exchange = elapsed + (self.exchange_ms or 0.0) * 1e-3
         if self.use_dist:
             dist.barrier(group=self.host_group)
             torch.cuda.synchronize(self.dev)
-            e = torch.tensor([elapsed], dtype=torch.float64)
+            e = torch.tensor([elapsed, self.elapsed_incl_exchange], dtype=torch.float64)
             dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.host_group)
-            elapsed = float(e.item())
+            elapsed, self.elapsed_incl_exchange = float(e[0].item()), float(e[1].item())
         return elapsed
 
     def roofline_leg(self, calls):
@@ -340,20 +348,29 @@ def reference_shaped(seconds):
 
 
 def early_exit_leg(dev, rank, world, config, n_per_gpu, steps, warmup, chunk, use_dist, host_group, check_oracle,
-                   first_chunk=None):
+                   first_chunk=None, plant=None):
     """BASELINE config 3's early-termination path: QSMD_FLAG_EARLY_EXIT_BATCH
     over a batch sharded across the ranks (qsmd.dist.check_shard_early_exit_device:
     device-resident shards, one MIN all-reduce of the first failure per
-    chunk, RCCL under torchrun).  One step = one early-exit pass over the
-    whole batch (n_per_gpu x world histories of the seeded stream); the
-    time is the MAX over ranks.  Reports the batch's histories per second
-    (every history decided: searched, or SKIPPED after the first failure as
-    QuickCheck stops at its first failing test, test/TicketDispenser.hs:284-322)
-    and the histories actually searched."""
+    round of geometrically growing chunks, RCCL under torchrun).  One step =
+    one early-exit pass over the whole batch (n_per_gpu x world histories of
+    the seeded stream): it ends when the batch is decided -- its first
+    failure found and every later history SKIPPED, as QuickCheck stops at its
+    first failing test (test/TicketDispenser.hs:284-322).  The time is the
+    MAX over ranks.  Reported as a latency, ms_to_decision, and as the
+    histories actually searched per second up to the decision (SKIPPED
+    histories are not work).  plant: a fraction f -- the histories are a
+    linearisable configuration's with one failure planted at f x the batch
+    (gen.plant_failure), so the rounds before it run for real."""
     from qsmd import dist as qdist
     n_total = n_per_gpu * world
     first, count = qdist.shard(n_total, rank, world)
     hdr, ev, _ = gen.generate(gen.params(**gen.CONFIGS[config]), first, count, threads=min(16, host_cores()))
+    planted = None
+    if plant is not None:
+        planted = min(n_total - 1, int(plant * n_total))
+        if first <= planted < first + count:
+            ev = gen.plant_failure(hdr, ev, planted - first)
     d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
     d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
     mid = gen.CONFIGS[config]["model_id"]
@@ -380,9 +397,10 @@ def early_exit_leg(dev, rank, world, config, n_per_gpu, steps, warmup, chunk, us
         dist.all_reduce(s, op=dist.ReduceOp.SUM, group=host_group)
         el, searched = float(e[0].item()), int(s.item())
     out = {"workload": config, "histories": n_total, "histories_per_gpu": n_per_gpu, "chunk": chunk,
-           "first_chunk": first_chunk, "steps": steps,
-           "ms_per_step": el / steps * 1e3, "histories_per_sec": n_total * steps / el,
-           "searched": searched, "searched_per_sec": searched * steps / el,
+           "first_chunk": first_chunk, "planted_at": planted, "steps": steps,
+           "ms_to_decision": el / steps * 1e3,
+           "searched": searched, "histories_searched_per_sec": searched * steps / el,
+           "skipped": n_total - searched,
            "first_fail": info["first_fail"], "rounds": info["rounds"],
            "totals": dict(zip(("checked", "linearisable", "nonlinearisable", "model_errors", "encode_errors",
                                "budget", "skipped", "nodes"), (int(x) for x in tot)))}
@@ -481,6 +499,9 @@ def main():
                     help="time BASELINE config 3's early-termination path instead (bank_4x16_bugs by default, "
                          "1.25M histories per GPU: 10M over 8 GPUs), sharded, QSMD_FLAG_EARLY_EXIT_BATCH")
     ap.add_argument("--chunk", type=int, default=262144, help="--early-exit: histories per rank per round (at most)")
+    ap.add_argument("--plant", type=float, default=None, metavar="F",
+                    help="--early-exit: config 2's linearisable stream with one failure planted at F x the batch "
+                         "(gen.plant_failure): the geometric rounds up to it run for real")
     ap.add_argument("--first-chunk", type=int, default=4096,
                     help="--early-exit: histories per rank in the first round, x4 per round up to --chunk "
                          "(qsmd.dist.early_chunks; 0: fixed --chunk rounds)")
@@ -557,17 +578,22 @@ def main():
     if args.early_exit:
         config = args.config if args.config != "bank_4x16" else "bank_4x16_bugs"
         n_ee = args.n_hist if args.n_hist != 1_000_000 else 1_250_000
+        if args.plant is not None and args.config == "bank_4x16":
+            config = "bank_4x16"             # (a linearisable stream: the planted failure is its only one)
         ee = early_exit_leg(dev, rank, world, config, n_ee, args.steps, args.warmup, args.chunk, use_dist, host_group,
-                            rank == 0 and not args.no_cpu_baseline, first_chunk=args.first_chunk or None)
+                            rank == 0 and not args.no_cpu_baseline, first_chunk=args.first_chunk or None,
+                            plant=args.plant)
         if rank == 0:
-            out = {"metric": "histories decided/sec, early-termination path (QSMD_FLAG_EARLY_EXIT_BATCH, sharded)",
-                   "value": ee["histories_per_sec"], "unit": "histories/s", "n_gpus": world, "steps": args.steps,
-                   "warmup": args.warmup, "ms_per_step": ee["ms_per_step"], "higher_is_better": True,
+            out = {"metric": "histories searched/sec up to the batch's decision, early-termination path "
+                             "(QSMD_FLAG_EARLY_EXIT_BATCH, sharded); ms_to_decision beside it",
+                   "value": ee["histories_searched_per_sec"], "unit": "histories/s", "n_gpus": world,
+                   "steps": args.steps, "warmup": args.warmup, "ms_per_step": ee["ms_to_decision"],
+                   "ms_to_decision": ee["ms_to_decision"], "higher_is_better": True,
                    "scaling": "weak", "vs_baseline": None, "dtype": "int32",
                    "data": "synthetic (seeded scheduler-policy generator with injected race bugs)",
                    "config": {"workload": config, "histories_per_gpu": n_ee, "parallelism": f"shard{world}",
                               "chunk": args.chunk, "first_chunk": args.first_chunk or None,
-                              "mode": "exhaustive + early exit"},
+                              "planted_at_fraction": args.plant, "mode": "exhaustive + early exit"},
                    "early_exit": ee}
             print(json.dumps(out), file=json_out, flush=True)
         if use_dist:
@@ -700,6 +726,9 @@ def main():
 
     out = {
         "metric": METRIC, "value": value, "unit": "histories/s", "n_gpus": world,
+        # the same histories over the window plus the counters' exchange after
+        # it (N > 1: the all-reduce of the totals; N = 1 exchanges nothing)
+        "value_incl_exchange": total_hist * args.steps / run.elapsed_incl_exchange,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32",
         "dtype_note": ("exact integer search: stage 0 holds invocation values in 9 bits (-256..255), responses "

@@ -167,10 +167,12 @@ uint32_t qsmd_abi_version(void);
  * a stream other than the previous call's first waits (on the device) for
  * that call, because they share the context's device workspace.  Calls that
  * should overlap use one context each (bench.py keeps calls in flight that
- * way).  Contexts share no device state.  The stream of a device call must
- * stay alive until the context's next check call, qsmd_close, or a host wait
- * of the context (qsmd_probe_read, qsmd_timed_out, a knob that reallocates):
- * those wait for that stream, never for the whole device. */
+ * way).  Contexts share no device state.  A device call on a caller's stream
+ * records a completion event on it, and the context's later waits (its next
+ * call on another stream, qsmd_close, qsmd_probe_read, qsmd_timed_out, a knob
+ * that reallocates) wait for that event, never for the caller's stream or the
+ * whole device: the caller may destroy its stream once its own work on it is
+ * done. */
 
 /* Check a batch held in HOST memory (the drop-in for one call per history;
  * n_hist = 1 is valid).  Buffers are copied in and out; the library keeps no

@@ -50,11 +50,11 @@ struct qsmd_ctx {
     // the calls of this context are ordered: each waits for the previous one
     // (whatever its stream), and buffers are freed only once it is done
     hipEvent_t done_ev = nullptr;
-    // the completion event is recorded only once the context has seen a
-    // second stream: a call's last packet costs a lone caller ~2-3 us (one
-    // call at a time 4.79-4.84 vs 4.71-4.76e9 without / with it,
-    // tools/gpu/r04_nodone.sh); on one stream the stream orders the calls
-    bool multi = false;                // calls on more than one stream: record done_ev every call
+    // A call on a caller's stream records the completion event, so that the
+    // context's later waits (quiesce, qsmd_close, a call on another stream)
+    // never name a stream the caller may have destroyed since; a call on the
+    // context's own stream (the host entry, which also waits for it before
+    // returning) does not need it
     bool done_last = false;            // the last call recorded done_ev
     hipStream_t last_stream = nullptr;
     bool in_flight = false;
@@ -90,7 +90,7 @@ struct qsmd_ctx {
     uint32_t* dag_dbg = nullptr;       // diagnostic (dag_debug_ptr / dag_debug_hist)
     uint64_t dag_dbg_h = 0;
     unsigned long long* wave_stats = nullptr;   // diagnostic (wave_stats_ptr): 16 x u64 (include/qsmd.h)
-    unsigned long long* memo_stats = nullptr;   // diagnostic (memo_stats_ptr): 8 x u64 per heavy-stage group
+    unsigned long long* memo_stats = nullptr;   // diagnostic (memo_stats_ptr): 16 x u64 per heavy-stage group
     uint64_t memo_stats_groups = 0;             // (memo_stats_groups)
     uint32_t memo_lds = 1;                      // heavy-stage memo tables in LDS: 0 never, 1 short lists, 2 always
     uint64_t giant_grid = 0;           // giant stage workgroups (0 = 2 per CU)
@@ -202,11 +202,10 @@ static bool sync_stages() {
 size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 
 // Wait until the context's previous call is done (its buffers may be in use):
-// its completion event, or (one stream so far, no event recorded) that
+// its completion event (a call on a caller's stream), or the context's own
 // stream -- never the whole device, which would wait for other contexts,
-// torch kernels and RCCL's streams too.  The stream of a device call must
-// therefore stay alive until the context's next call, qsmd_close, or a host
-// wait of this context (include/qsmd.h).
+// torch kernels and RCCL's streams too, and never a caller's stream, which
+// the caller may destroy once its own work on it is done.
 void quiesce(qsmd_ctx* c) {
     if (c->in_flight) {
         if (c->done_last) (void)hipEventSynchronize(c->done_ev);
@@ -216,13 +215,11 @@ void quiesce(qsmd_ctx* c) {
 }
 
 // A call on stream s: the previous call of this context (on another
-// stream) comes first -- its completion event, or, the first time a second
-// stream shows up (no event recorded yet), a host wait for the previous
-// stream; every call records the event from then on.
+// stream) comes first -- its completion event, or a host wait for the
+// context's own stream.
 static hipError_t order_after_previous(qsmd_ctx* c, hipStream_t s) {
-    if (!c->in_flight || c->last_stream == s) return hipSuccess;
-    c->multi = true;
-    if (c->done_last) return hipStreamWaitEvent(s, c->done_ev, 0);
+    if (!c->in_flight || (c->last_stream == s && !c->done_last)) return hipSuccess;
+    if (c->done_last) return c->last_stream == s ? hipSuccess : hipStreamWaitEvent(s, c->done_ev, 0);
     const hipError_t e = hipStreamSynchronize(c->last_stream);
     if (e == hipSuccess) c->in_flight = false;
     return e;
@@ -429,7 +426,7 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->wave_min_rem = std::min<uint64_t>(value, 0xFFFFFFFFull);
     } else if (n == "wave_stats_ptr") {     // diagnostic: device buffer of 16 x u64 (zeroed by the caller)
         c->wave_stats = reinterpret_cast<unsigned long long*>(value);
-    } else if (n == "memo_stats_ptr") {     // diagnostic: device buffer of 8 x u64 per heavy-stage group (zeroed)
+    } else if (n == "memo_stats_ptr") {     // diagnostic: device buffer of 16 x u64 per heavy-stage group (zeroed)
         c->memo_stats = reinterpret_cast<unsigned long long*>(value);
     } else if (n == "memo_stats_groups") {
         c->memo_stats_groups = value;
@@ -895,8 +892,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     stage_done("giants", s, cnt);
     c->ws_dirty = false;
     if (tm) HIP_TRY(c, hipEventRecord(evs[2], s), "hipEventRecord");
-    if (c->multi) HIP_TRY(c, hipEventRecord(c->done_ev, s), "hipEventRecord");
-    c->done_last = c->multi;
+    const bool own = s == c->stream;
+    if (!own) HIP_TRY(c, hipEventRecord(c->done_ev, s), "hipEventRecord");
+    c->done_last = !own;
     c->last_stream = s;
     c->in_flight = true;
     c->any_call = true;

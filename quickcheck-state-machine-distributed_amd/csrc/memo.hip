@@ -49,47 +49,71 @@ template <uint32_t MODEL, class G>
 struct LaneKey {
     uint32_t w1, rem_lo, rem_hi, m[4];
     uint32_t slot;
-    bool ok;
 };
 
-// the key of the lane's current state (the node at depth dfs.depth)
+// The memo's slot hash: slot = the top log2(entries) bits of one
+// multiplicative hash (they see every input bit): product >> sh,
+// sh = 32 - log2(entries) (entries >= 2).
+struct SlotHash {
+    uint32_t sh;
+};
+
+// Whether every state a search of this call can reach has a memo key: the
+// key holds balances (Bank) or the counter (Ticket) as i16, and a compact
+// history of at most G::LEVELS operations with values of 9 bits (c_ival)
+// moves an account by at most 256 per operation, so a model0 within
+// +-(32767 - 256 LEVELS) keeps every reachable state in range.  Checked once
+// per call (wave-uniform) instead of per node; a call outside it runs the
+// memo stage without the memo (exact either way).
+template <uint32_t MODEL, class G>
+__device__ __forceinline__ bool keys_fit(const SearchArgs& a) {
+    constexpr int64_t lim = 32767 - 256 * G::LEVELS;
+    bool ok = true;
+    if constexpr (MODEL == QSMD_MODEL_BANK) {
+#pragma unroll
+        for (int q = 0; q < QSMD_BANK_MAX_ACCOUNTS; ++q)
+            ok = ok && (!((a.m0_exists >> q) & 1u) || (a.m0_val[q] >= -lim && a.m0_val[q] <= lim));
+    } else {
+        ok = !a.m0_just || (a.m0_val[0] >= -lim && a.m0_val[0] <= lim);
+    }
+    return ok;
+}
+
+// the key of the lane's current state (the node at depth dfs.depth); the
+// caller has checked keys_fit
 template <uint32_t MODEL, class G>
 __device__ __forceinline__ LaneKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d, const SearchArgs& a,
                                                       int32_t (*s_bal)[C_LANES], int lane, uint32_t epoch,
-                                                      uint32_t mask) {
+                                                      SlotHash sh) {
     LaneKey<MODEL, G> k;
-    k.ok = true;
     k.rem_lo = (uint32_t)d.rem;
     k.rem_hi = G::EV == 64 ? (uint32_t)((uint64_t)d.rem >> 32) : 0u;
     uint32_t ex = 0;
     if constexpr (MODEL == QSMD_MODEL_BANK) {
         ex = d.ex;
         // an absent account holds 0 in LDS (LaneDFS: created from 0, restored
-        // to 0 by undo), so the balances are read unconditionally
+        // to 0 by undo), so the balances are read unconditionally; two i16
+        // halves per word by one v_perm
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int32_t b0 = s_bal[2 * q][lane];
-            const int32_t b1 = s_bal[2 * q + 1][lane];
-            k.ok = k.ok && b0 == (int32_t)(int16_t)b0 && b1 == (int32_t)(int16_t)b1;
-            k.m[q] = ((uint32_t)b0 & 0xFFFFu) | ((uint32_t)b1 << 16);
-        }
+        for (int q = 0; q < 4; ++q)
+            k.m[q] = __builtin_amdgcn_perm((uint32_t)s_bal[2 * q + 1][lane], (uint32_t)s_bal[2 * q][lane],
+                                           0x05040100u);
     } else {
         // model after the levels 0 .. depth-1 (the formula of LaneDFS::try_next)
         const uint32_t just = d.RS ? 1u : a.m0_just;
         const int32_t n = d.RS ? (int32_t)(d.depth - 1u - (31u - __builtin_clz(d.RS | 1u)))
                                : (int32_t)a.m0_val[0] + (a.m0_just ? (int32_t)d.depth : 0);
-        k.ok = !just || n == (int32_t)(int16_t)n;
         k.m[0] = just | (just ? ((uint32_t)n & 0xFFFFu) << 1 : 0u);
         k.m[1] = k.m[2] = k.m[3] = 0u;
     }
     k.w1 = (epoch & 0xFFFFFFu) | (ex << 24);
-    // slot: three independent multiplicative hashes, folded (a short
-    // dependent chain: the key is computed twice per DFS iteration)
-    const uint32_t v = (k.m[0] ^ __builtin_amdgcn_alignbit(k.m[1], k.m[1], 8)) ^
+    // the model words rotated apart and folded into the remaining set, then
+    // one multiplicative hash (one quarter-rate multiply per key)
+    const uint32_t v = (k.m[0] ^ ex ^ __builtin_amdgcn_alignbit(k.m[1], k.m[1], 8)) ^
                        (__builtin_amdgcn_alignbit(k.m[2], k.m[2], 16) ^ __builtin_amdgcn_alignbit(k.m[3], k.m[3], 24));
-    uint32_t h = (k.rem_lo * 0x9E3779B1u) ^ ((k.rem_hi ^ ex) * 0x85EBCA77u) ^ (v * 0xC2B2AE3Du);
-    h ^= (h >> 16) ^ (h >> 24);   // the low bits see every input bit through the products' top bits
-    k.slot = h & mask;
+    uint32_t t = k.rem_lo ^ __builtin_amdgcn_alignbit(v, v, 13);
+    if constexpr (G::EV == 64) t ^= __builtin_amdgcn_alignbit(k.rem_hi, k.rem_hi, 7);
+    k.slot = (t * 0x9E3779B1u) >> sh.sh;
     return k;
 }
 
@@ -168,14 +192,49 @@ struct Written {
     __device__ __forceinline__ bool maybe(uint32_t slot) const { return (m >> (slot & 63u)) & 1ull; }
 };
 
+// Diagnostic (ST) records per group: kMemoStatsWords u64 (tools/memo_stats.py).
+//   [0..2] realtime at start / staged / end  [3] max DFS iterations over the
+//   lanes  [4] their sum  [5] memo hits  [6] histories  [7] shader cycles of
+//   the search loop (max over the lanes)
+//   [8..12] shader cycles the wavefront spent in the iteration's phases, each
+//   drained of its memory operations before its end stamp (so latency lands
+//   in the phase that issued it): [8] backtrack (entry count, memo count,
+//   undo) [9] try_next [10] memo key [11] HBM probe [12] hit / pending
+//   entry / level record
+//   [13] wave iterations with a backtrack [14] with an HBM probe [15] wave
+//   iterations
+constexpr uint32_t kMemoStatsWords = 16;
+
+// One wavefront per workgroup: phase clocks in LDS, added by one lane
+// (the first active one of the block that stamps).
+struct PhaseClock {
+    uint64_t acc[8];
+    __device__ __forceinline__ uint64_t start() {
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+        return t;
+    }
+    __device__ __forceinline__ void stop(int k, uint64_t t0, int lane) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt(0);
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+        if (lane == (int)__builtin_ctzll(__ballot(1))) acc[k] += t - t0;
+    }
+    __device__ __forceinline__ void count(int k, bool any, int lane) {
+        if (lane == 0 && any) acc[k] += 1;
+    }
+};
+
 // One DFS iteration with the memo (LaneDFS::step plus the two hooks).
 // entry: the lane's column of node counts at entry, per level; tab: the
 // lane's HBM table, or (LT) its LDS column.
-template <uint32_t MODEL, class G, bool LT>
+template <uint32_t MODEL, class G, bool LT, bool ST>
 __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* evc,
                                          int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* tab,
-                                         uint32_t h, uint32_t epoch, uint32_t mask, uint32_t* entry, bool& skip,
-                                         uint64_t memo_after, Written& wr) {
+                                         uint32_t h, uint32_t epoch, SlotHash sh, uint32_t* entry, bool& skip,
+                                         uint64_t memo_after, Written& wr, PhaseClock* ph) {
     using M = typename G::M;
     // a short search runs as the plain DFS (no HBM probe per node); the memo
     // joins once the search has counted memo_after nodes (entry counts are
@@ -186,16 +245,22 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     const bool term = empty & ((d.found == 0u) | (d.depth == d.base));
     int status = !term ? -1
                        : ((!d.found && d.depth > 0) ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE);
+    uint64_t t0 = 0;
+    if constexpr (ST) {
+        ph->count(5, __ballot(empty & !term) != 0ull, lane);
+        ph->count(7, true, lane);
+    }
     if (empty & !term) {
+        if constexpr (ST) t0 = ph->start();
         // leaving the node at depth d.depth: its subtree was searched to the end and failed
         // (counts kept mod 2^32: exact while the running count is below 2^32)
         // (the level's entry count and the key's balances read together:
         // gating the key on the entry count put its LDS round trip first)
         const uint32_t ent = entry[(d.depth - 1u) * C_LANES];
         if (memo && !skip && d.nodes <= 0xFFFFFFFFull) {
-            const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
+            const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, sh);
             const uint32_t cnt = (uint32_t)d.nodes - ent;
-            if (k.ok && ent != kNoEntry) {
+            if (ent != kNoEntry) {
                 if constexpr (LT) {
                     memo_insert_lds<MODEL, G>(tab, k, h, cnt);
                 } else {
@@ -208,21 +273,31 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
         const uint32_t j = d.template undo<C_LANES>(evc, s_bal, lane);
         d.cand = cands(d.rem, d.INV, d.RESP) & mask_above(j, (M)0);
         d.found = 1u;
+        if constexpr (ST) ph->stop(0, t0, lane);
     }
     if (d.cand) {
         const uint32_t dep0 = d.depth;
+        if constexpr (ST) t0 = ph->start();
         status = d.template try_next<C_LANES>(a, evc, s_bal, lane, limit);
+        if constexpr (ST) ph->stop(1, t0, lane);
         if (d.depth > dep0 && status < 0) {       // entered a new node (and the search goes on)
             entry[dep0 * C_LANES] = (uint32_t)d.nodes;
         }
         if (memo && d.depth > dep0 && status < 0) {
-            const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, mask);
+            if constexpr (ST) t0 = ph->start();
+            const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, sh);
+            if constexpr (ST) ph->stop(2, t0, lane);
             uint32_t cnt = 0;
             bool hit = false;
             if constexpr (LT) {
-                if (k.ok) hit = memo_lookup_lds<MODEL, G>(tab, k, h, cnt);
+                hit = memo_lookup_lds<MODEL, G>(tab, k, h, cnt);
             } else {
-                if (k.ok && wr.maybe(k.slot)) hit = memo_lookup<MODEL, G>(tab, k, h, cnt);
+                if constexpr (ST) ph->count(6, __ballot(wr.maybe(k.slot)) != 0ull, lane);
+                if (wr.maybe(k.slot)) {
+                    if constexpr (ST) t0 = ph->start();
+                    hit = memo_lookup<MODEL, G>(tab, k, h, cnt);
+                    if constexpr (ST) ph->stop(3, t0, lane);
+                }
             }
             if (hit) {
                 if (d.nodes + cnt > limit) {      // the budget falls inside that subtree
@@ -254,8 +329,7 @@ struct MemoLds {
 // One group of 64 histories of p's list (from index base); every history of
 // the list fits geometry G (a compact stage staged it before).
 // ST: diagnostic build of the loop, one record per group in p.stats
-// (realtime at start / staged / end, max and summed DFS iterations over the
-// lanes, memo hits, histories, shader cycles of the search loop).
+// (kMemoStatsWords: see PhaseClock).
 template <uint32_t MODEL, class G, bool LT, bool ST>
 __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, MemoLds<MODEL, G>& L, uint32_t* lcol,
                                            Counters& cnt, uint64_t t0, int lane, unsigned long long* q) {
@@ -264,15 +338,17 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
     const uint64_t total = list_total(a.list_count, a.list_shard_cap);
     const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
     uint32_t* tab;
-    uint32_t mask;
+    SlotHash sh;
     if constexpr (LT) {
         tab = lcol;
-        mask = p.lds_entries - 1u;
+        sh.sh = 32u - (uint32_t)__builtin_ctz(p.lds_entries);
     } else {
         tab = p.table + ((uint64_t)blockIdx.x * C_LANES + (uint64_t)lane) * (uint64_t)p.entries *
                             (uint64_t)MemoEntry<G>::W;
-        mask = p.entries - 1u;
+        sh.sh = 32u - (uint32_t)__builtin_ctz(p.entries);
     }
+    // a call with a model0 some reachable state has no key for: no memo
+    const uint64_t memo_after = keys_fit<MODEL, G>(a) ? (uint64_t)p.memo_after : ~0ull;
     const uint64_t idx = base + lane;
     const bool active = idx < total;
     uint64_t r0 = 0, c0 = 0;
@@ -334,6 +410,13 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
         uint32_t lane_iter = 0;   // (ST only)
         Written wr;
         wr.clear();
+        PhaseClock* ph = nullptr;
+        if constexpr (ST) {
+            __shared__ PhaseClock phc;
+            ph = &phc;
+            if (lane == (int)__builtin_ctzll(__ballot(1)))
+                for (int k = 0; k < 8; ++k) phc.acc[k] = 0;
+        }
         // nothing outstanding at the loop's entry: otherwise the compiler
         // waits for the memo insert's stores inside the loop (vmcnt counts
         // them), a store round trip on every backtrack
@@ -344,8 +427,8 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
             while (k < span) {
                 if (status < 0) {
                     const bool was = skip;
-                    status = memo_step<MODEL, G, LT>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h, p.epoch,
-                                                     mask, &L.entry[0][lane], skip, p.memo_after, wr);
+                    status = memo_step<MODEL, G, LT, ST>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h,
+                                                         p.epoch, sh, &L.entry[0][lane], skip, memo_after, wr, ph);
                     if constexpr (ST) {
                         hits += (!was && skip) ? 1u : 0u;
                         ++lane_iter;
@@ -374,6 +457,8 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
             atomicAdd(q + 4, (unsigned long long)lane_iter);
             atomicAdd(q + 5, (unsigned long long)hits);
             atomicMax(q + 7, (unsigned long long)(__builtin_amdgcn_s_memtime() - c0));
+            if (lane == (int)__builtin_ctzll(__ballot(1)))
+                for (int k = 0; k < 8; ++k) atomicAdd(q + 8 + k, (unsigned long long)ph->acc[k]);
         }
     }
     if constexpr (ST) {
@@ -426,7 +511,8 @@ __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32,
         wave_append(in, in ? p32.fwd_list[b + lane] : 0u, p32.s.giant_list, p32.s.giant_count, lane);
     }
     for (uint64_t grp = blockIdx.x; grp < n32 + n64; grp += gridDim.x) {
-        unsigned long long* q = p32.stats && grp < p32.stats_groups ? p32.stats + grp * 8u : nullptr;
+        unsigned long long* q =
+            p32.stats && grp < p32.stats_groups ? p32.stats + grp * kMemoStatsWords : nullptr;
         if (grp < n32) {
             auto& L = *reinterpret_cast<MemoLds<MODEL, G32>*>(lds);
             if (q) memo_group<MODEL, G32, LT, true>(p32, grp * 64u, L, lcol, cnt, t0, lane, q);

@@ -119,6 +119,20 @@ def adversarial_ticket(n_clients=8, n_ops=64, bug=True):
     return hdr, events, np.array([1 if bug else 0], dtype=np.uint8)
 
 
+def plant_failure(hdr, events, i):
+    """A copy of `events` in which history i fails: its last response becomes
+    `Balance 2^20` (Bank), a value no interleaving explains -- the injected
+    race bug of the early-exit leg's planted stream (bench.py --plant, tests
+    test_distributed.py).  The history keeps its shape."""
+    ev = events.copy()
+    o, n = int(hdr[i]["ev_off"]), int(hdr[i]["n_ev"])
+    resp = [k for k in range(o, o + n) if ev["kp"][k] & 0x80]
+    k = resp[-1]
+    ev["code"][k] = 7                                   # Balance
+    ev["val"][k] = 1 << 20
+    return ev
+
+
 def generate_config(name, first, n_hist, threads=8, **override):
     kw = dict(CONFIGS[name])
     kw.update(override)

@@ -118,12 +118,7 @@ def planted_stream(config, n_total, plant):
     from qsmd import gen
     hdr, ev, _ = gen.generate(gen.params(**gen.CONFIGS[config]), 0, n_total)
     if plant is not None:
-        ev = ev.copy()
-        o, n = int(hdr[plant]["ev_off"]), int(hdr[plant]["n_ev"])
-        resp = [k for k in range(o, o + n) if ev["kp"][k] & 0x80]
-        k = resp[-1]                                  # the last response: a value nothing else can explain
-        ev["code"][k] = 7                             # Balance
-        ev["val"][k] = 1 << 20
+        ev = gen.plant_failure(hdr, ev, plant)        # the last response: a value nothing else can explain
     return hdr, ev
 
 

@@ -32,3 +32,35 @@ def test_bench_one_gpu_with_extra_configs():
     for k in ("config1", "config3", "config5"):
         assert ex[k]["mismatches_vs_oracle"] == 0 and ex[k]["histories_per_sec"] > 0
     assert ex["config4"]["verdict_matches_oracle"]
+
+
+@pytest.mark.parametrize("plant", [None, 0.6])
+def test_bench_early_exit_leg(plant):
+    """The early-exit leg on one GPU: config 3 (its first failure is its
+    second history: one round decides) and config 2's stream with one
+    failure planted at 60 % of the batch (the geometric rounds up to it, a
+    MIN per round): the decision's latency, the histories searched, and the
+    statuses against the oracle cut (every history up to the first failure
+    the oracle's, every later one SKIPPED)."""
+    n = 60000
+    cmd = [sys.executable, "bench.py", "--early-exit", "--steps", "2", "--warmup", "1", "--n-hist", str(n)]
+    if plant is not None:
+        cmd += ["--plant", str(plant)]
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=200,
+                       env=dict(os.environ, PYTHONUNBUFFERED="1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    ee = d["early_exit"]
+    assert d["ms_to_decision"] == ee["ms_to_decision"] > 0
+    assert d["value"] == ee["histories_searched_per_sec"] > 0
+    assert ee["mismatches_vs_oracle"] == 0
+    assert ee["searched"] + ee["skipped"] == n
+    if plant is None:
+        assert ee["workload"] == "bank_4x16_bugs" and ee["rounds"] == 1 and ee["first_fail"] < 4096
+    else:
+        at = int(plant * n)
+        assert ee["workload"] == "bank_4x16" and ee["planted_at"] == at == ee["first_fail"]
+        assert ee["rounds"] > 2 and ee["searched"] >= at + 1
+        assert ee["totals"]["nonlinearisable"] + ee["totals"]["model_errors"] == 1

@@ -227,6 +227,12 @@ def test_bench_two_ranks_on_one_gpu():
     assert d["n_gpus"] == 2 and d["steps"] == 6 and d["value"] > 0
     assert d["verdicts"]["checked"] + d["verdicts"]["budget"] <= 2 * 6 * 20000
     assert "gloo" in d["config"]["counters"] and d["config"]["exchange_ms"] is not None
+    # the headline with the exchange inside: the same histories over the
+    # window plus exchange_ms (MAX over the ranks of each)
+    assert 0 < d["value_incl_exchange"] < d["value"]
+    t_win = 2 * 6 * 20000 / d["value"]
+    assert abs(2 * 6 * 20000 / d["value_incl_exchange"] - t_win - d["config"]["exchange_ms"] * 1e-3) \
+        < 0.5 * t_win + 0.05
 
 
 @pytest.mark.parametrize("n_total,plant,chunk,first_chunk", [

@@ -6,6 +6,7 @@ itself pinned to the literal list transliteration and the KATs
 (tests/test_oracle.py).
 """
 
+import ctypes
 import random
 
 import numpy as np
@@ -260,7 +261,22 @@ def test_lane_mode_memo_after(ctx, knobs, name, n, budget, max_nodes, memo_after
     _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
 
 
-LANE_CASES = [("bank_4x16_bugs", 50000, 64, 0), ("bank_4x16_bugs", 20000, 8, 300), ("bank_4x16", 50000, 16, 0),
+@pytest.mark.parametrize("bal", [28671, 28672, -28671, -28672, 200000])
+@pytest.mark.parametrize("lds", [0, 2])
+def test_lane_mode_key_range(ctx, knobs, bal, lds):
+    """Lane mode keys a state's balances as i16; a 16-operation history moves
+    an account by at most 16 x 256, so a model0 within +-28671 keeps every
+    reachable state keyable and the memo runs, and one beyond it turns the
+    memo off for the call (memo.hip keys_fit) -- exact either way: the
+    reference's verdicts, node counts and witnesses on both sides of the
+    bound, with HBM and LDS tables."""
+    knobs(heavy_mode=1, memo_lds=lds, stage0_budget=8, stage0w_budget=8, memo_after=1)
+    hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 21, 20000)
+    m0 = models.BankModel(0b1111, 0, (ctypes.c_int64 * 8)(bal, 7, -bal // 3, 0, 0, 0, 0, 0))
+    _compare(ctx, models.MODEL_BANK, hdr, ev, m0, max_nodes=10**7)
+
+
+LANE_CASES = [("bank_4x16_bugs", 50000, 64, 0),("bank_4x16_bugs", 20000, 8, 300), ("bank_4x16", 50000, 16, 0),
               ("ticket_2x10", 20000, 4, 0), ("bank_6x24", 20000, 16, 0), ("bank_6x24", 20000, 8, 500)]
 
 
@@ -660,50 +676,56 @@ def test_device_resident_full_size(ctx, name, n):
 
 @pytest.mark.parametrize("name,n", [("bank_4x16", 1_000_000), ("bank_4x16_bugs", 1_250_000)])
 def test_bench_knobs_in_flight_full_size(name, n):
-    """bench.py's own knob set at full size: stage-0 budget 18, the heavy
-    stage in lane mode with HBM memo tables (heavy_mode 1, memo_lds 0), three
-    contexts on three streams with calls in flight (each context's second
-    call sizes its tail grids and lane tables from its first), on config 2
-    (1M) and on config 3's per-GPU share of 10M over 8 GPUs (1.25M): every
-    status and node count of every call equals the oracle's
+    """bench.py's own knob set at full size: stage-0 budget 20, the heavy
+    stage in lane mode with HBM memo tables (heavy_mode 1, memo_lds 0), four
+    contexts on four streams with calls in flight, five distinct resident
+    batches in rotation (step k checks batch k % 5 on slot k % 4, so every
+    context's tail grids and lane tables come from another batch's call), on
+    config 2 (1M per batch) and on config 3's per-GPU share of 10M over 8 GPUs
+    (1.25M): every status and node count of every call equals the oracle's
     (/root/reference/test/Bank.hs:256-287 checks one history per call)."""
     torch = pytest.importorskip("torch")
+    S, K, steps = 4, 5, 10
     mid = gen.CONFIGS[name]["model_id"]
-    hdr, ev, _ = gen.generate_config(name, 0, n)
     dev = torch.device("cuda:0")
-    d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
-    d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
-    ctxs = [device.Context(0, time_limit_ms=60000) for _ in range(3)]
-    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    host, batches = [], []
+    for k in range(K):
+        hdr, ev, _ = gen.generate(gen.params(**gen.CONFIGS[name]), k * n, n, threads=16)
+        host.append((hdr, ev))
+        batches.append((torch.from_numpy(hdr.view(np.uint8)).to(dev), torch.from_numpy(ev.view(np.uint8)).to(dev),
+                        len(ev)))
+    ctxs = [device.Context(0, time_limit_ms=60000) for _ in range(S)]
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]
     outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev),
-             torch.zeros(8, dtype=torch.int64, device=dev)) for _ in range(3)]
+             torch.zeros(8, dtype=torch.int64, device=dev)) for _ in range(steps)]
+    torch.cuda.synchronize()
     try:
         for c in ctxs:
-            c.set_stage0_budget(18)
+            c.set_stage0_budget(20)
             c.set_param("heavy_mode", 1)
             c.set_param("memo_lds", 0)
-        results = []
-        for rnd in range(2):
-            for i in range(3):
-                d_st, d_nd, d_tot = outs[i]
-                with torch.cuda.stream(streams[i]):
-                    d_st.fill_(0xEE)
-                    ctxs[i].check_device(mid, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), d_st.data_ptr(),
-                                         d_nd.data_ptr(), None, d_tot.data_ptr(), flags=device.QSMD_FLAG_EXHAUSTIVE,
-                                         stream=streams[i].cuda_stream)
-            torch.cuda.synchronize()
-            results += [(o[0].cpu().numpy(), o[1].cpu().numpy().astype(np.uint64), o[2].cpu().numpy())
-                        for o in outs]
+        for k in range(steps):
+            i = k % S
+            d_hdr, d_ev, n_ev = batches[k % K]
+            d_st, d_nd, d_tot = outs[k]
+            with torch.cuda.stream(streams[i]):
+                d_st.fill_(0xEE)
+                ctxs[i].check_device(mid, d_hdr.data_ptr(), n, d_ev.data_ptr(), n_ev, d_st.data_ptr(),
+                                     d_nd.data_ptr(), None, d_tot.data_ptr(), flags=device.QSMD_FLAG_EXHAUSTIVE,
+                                     stream=streams[i].cuda_stream)
+        torch.cuda.synchronize()
+        results = [(o[0].cpu().numpy(), o[1].cpu().numpy().astype(np.uint64), o[2].cpu().numpy()) for o in outs]
     finally:
         for c in ctxs:
             c.close()
-    st_o, nd_o, _ = oracle_c.check_batch(mid, hdr, ev, threads=16)
-    for st, nd, tot in results:
+    oracle = [oracle_c.check_batch(mid, hdr, ev, threads=16)[:2] for hdr, ev in host]
+    for k, (st, nd, tot) in enumerate(results):
+        st_o, nd_o = oracle[k % K]
         bad = np.nonzero((st != st_o) | (nd != nd_o))[0]
-        assert len(bad) == 0, f"{len(bad)} mismatches, first {bad[:5]}"
+        assert len(bad) == 0, f"step {k}: {len(bad)} mismatches, first {bad[:5]}"
         assert int(tot[0]) == int((st <= 2).sum()) and int(tot[7]) == int(nd.sum())
     if name == "bank_4x16":
-        assert (st_o == codec.STATUS_LIN).all()
+        assert all((o[0] == codec.STATUS_LIN).all() for o in oracle)
 
 
 @pytest.mark.parametrize("packed", [True, False])
@@ -823,6 +845,45 @@ def test_host_waits_stay_with_the_context():
     finally:
         A.close()
         B.close()
+
+
+def test_caller_streams_destroyed_between_calls():
+    """A plain HIP caller's lifetime pattern: create a stream, make a device
+    call on it, synchronise it, destroy it -- then the next call on a new
+    stream, a host wait of the context (qsmd_probe_read), qsmd_close.  The
+    context waits on its completion event (ABI 3), never on the
+    destroyed stream handle.  Results equal the oracle's."""
+    torch = pytest.importorskip("torch")
+    import ctypes
+    dev = torch.device("cuda:0")
+    hip = ctypes.CDLL("libamdhip64.so.7")     # (the runtime torch and libqsmd.so already share)
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 5, 20000)
+    n = len(hdr)
+    d_hdr = torch.from_numpy(hdr.view(np.uint8)).to(dev)
+    d_ev = torch.from_numpy(ev.view(np.uint8)).to(dev)
+    outs = [(torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
+            for _ in range(3)]
+    torch.cuda.synchronize()
+    st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr, ev, None, 10**7, 8)
+    A = device.Context(0)
+    try:
+        for k, (st, nd) in enumerate(outs):
+            s = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+            A.check_device(models.MODEL_BANK, d_hdr.data_ptr(), n, d_ev.data_ptr(), len(ev), st.data_ptr(),
+                           nd.data_ptr(), None, None, max_nodes=10**7, stream=s.value)
+            assert hip.hipStreamSynchronize(s) == 0
+            assert hip.hipStreamDestroy(s) == 0
+            if k == 1:
+                A.probe()                        # a host wait after the stream is gone
+        for st, nd in outs:
+            assert np.array_equal(st.cpu().numpy(), st_o)
+            assert np.array_equal(nd.cpu().numpy().astype(np.uint64), nd_o.astype(np.uint64))
+    finally:
+        A.close()                                # (the last call's stream destroyed too)
 
 
 def test_packed_lookalike_layouts(ctx):

@@ -210,11 +210,17 @@ def test_adversarial_ticket_exhaustive_split(ctx):
 @pytest.mark.parametrize("bug", [True, False])
 def test_adversarial_ticket_memo(ctx, bug):
     """BASELINE config 4: 8 clients x 64 ops, shared pid, heavy overlap;
-    (8!)^7 paths without memo, a few hundred states with it."""
+    (8!)^7 paths without memo, a few hundred states with it.  Memo mode's
+    node count is the pruning DFS's explored count (oracle/ref_cpu.c: each
+    state's children evaluated once): equal to the oracle's (281 with the
+    bug)."""
     h, e, _ = gen.adversarial_ticket(8, 64, bug=bug)
-    st_o, _, w_o = oracle_c.check_batch(models.MODEL_TICKET, h, e, memo=True, witness=True)
+    st_o, nd_o, w_o = oracle_c.check_batch(models.MODEL_TICKET, h, e, memo=True, witness=True)
     st, nd, w, _ = ctx.check_arrays(models.MODEL_TICKET, h, e, flags=EXH | MEMO, witness=True)
     assert int(st[0]) == int(st_o[0]) == (codec.STATUS_NONLIN if bug else codec.STATUS_LIN)
+    assert int(nd[0]) == int(nd_o[0]), (int(nd[0]), int(nd_o[0]))
+    if bug:
+        assert int(nd[0]) == 281
     if not bug:
         assert np.array_equal(w, w_o)
 

@@ -29,14 +29,16 @@ def main():
                 print(out.stderr[-2000:], file=sys.stderr)
                 sys.exit(out.returncode)
             d = json.loads(out.stdout.strip().splitlines()[-1])
-            row = (d["value"] / 1e9, d["device_ms"]["stage0_mean"], d["device_ms"]["call_mean"])
+            al = d["device_ms"]["alone"]
+            row = (d["value"] / 1e9, al["stage0_mean"], al["heavy_mean"] or 0.0, al["call_mean"])
             res[lib].append(row)
-            print(f"round {r} {os.path.basename(lib)}: value {row[0]:.3f}e9 stage0 {row[1]:.4f} ms "
-                  f"call {row[2]:.4f} ms", flush=True)
+            print(f"round {r} {os.path.basename(lib)}: value {row[0]:.3f}e9 alone: stage0 {row[1]:.4f} ms "
+                  f"heavy {row[2]:.4f} ms call {row[3]:.4f} ms", flush=True)
     for lib in libs:
         v = list(zip(*res[lib]))
-        print(f"MEDIAN {os.path.basename(lib)}: value {statistics.median(v[0]):.3f}e9 stage0 "
-              f"{statistics.median(v[1]):.4f} ms call {statistics.median(v[2]):.4f} ms", flush=True)
+        print(f"MEDIAN {os.path.basename(lib)}: value {statistics.median(v[0]):.3f}e9 alone: stage0 "
+              f"{statistics.median(v[1]):.4f} ms heavy {statistics.median(v[2]):.4f} ms call "
+              f"{statistics.median(v[3]):.4f} ms", flush=True)
 
 
 if __name__ == "__main__":

@@ -1,7 +1,10 @@
 """Heavy-stage (lane mode) diagnostics on a generated configuration: per
 group of 64 histories, the wall time from its start to its staging and to its
 last history, the DFS iterations of its longest lane, memo hits and shader
-cycles per iteration (memo_stats_ptr; one diagnostic call after warm-up).
+cycles per iteration, and the wavefront's cycles per iteration in each phase
+of the DFS step (memo_stats_ptr, memo.hip PhaseClock: each phase drained of
+its memory operations before its end stamp, so the phases add up to more
+than the undrained loop; one diagnostic call after warm-up).
 
     python tools/memo_stats.py bank_4x16 1000000 [param=value ...]
 """
@@ -32,7 +35,8 @@ def main():
     d_st = torch.empty(n, dtype=torch.uint8, device=dev)
     d_nd = torch.empty(n, dtype=torch.int64, device=dev)
     groups = (n + 63) // 64
-    stats = torch.zeros(groups * 8, dtype=torch.int64, device=dev)
+    W = 16                                  # u64 per group (memo.hip kMemoStatsWords)
+    stats = torch.zeros(groups * W, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def call():
@@ -49,7 +53,7 @@ def main():
     torch.cuda.synchronize()
     ctx.set_param("memo_stats_ptr", 0)
     s0, dev_ms = ctx.timing_read()
-    q = stats.view(groups, 8).cpu().numpy().astype(np.int64)
+    q = stats.view(groups, W).cpu().numpy().astype(np.int64)
     q = q[q[:, 6] > 0]
     if len(q) == 0:
         print(json.dumps({"groups": 0}))
@@ -82,6 +86,18 @@ def main():
                           "span_us": round(float(span[worst]), 1), "max_iterations": int(q[worst, 3]),
                           "histories": int(q[worst, 6])},
     }
+    wave_it = max(int(q[:, 15].sum()), 1)
+    names = ("backtrack", "try_next", "memo_key", "hbm_probe", "hit_insert_level")
+    out["phase_cycles_per_wave_iteration"] = {k: round(float(q[:, 8 + i].sum()) / wave_it, 0)
+                                              for i, k in enumerate(names)}
+    out["wave_iterations"] = wave_it
+    out["fraction_of_wave_iterations"] = {"with_backtrack": round(float(q[:, 13].sum()) / wave_it, 3),
+                                          "with_hbm_probe": round(float(q[:, 14].sum()) / wave_it, 3)}
+    lw = worst
+    wl = max(int(q[lw, 15]), 1)
+    out["longest_group"]["phase_cycles_per_iteration"] = {k: round(float(q[lw, 8 + i]) / wl, 0)
+                                                          for i, k in enumerate(names)}
+    out["longest_group"]["with_hbm_probe"] = round(float(q[lw, 14]) / wl, 3)
     print(json.dumps(out), flush=True)
     ctx.close()
 
