@@ -14,8 +14,11 @@ ranks (64 B) follows the window, timed on its own (config.exchange_ms).
 Environment (diagnostics): QSMD_BENCH_DIST=1 runs one rank on the N > 1
 path; QSMD_BENCH_COUNTERS=rccl exchanges the counters over RCCL inside the
 window instead, =gloo on the host after it; QSMD_BENCH_HOSTTIME=1 prints the window's host-time split
-on stderr; QSMD_BENCH_DEVICE=d pins every rank to GPU d; QSMD_LIB_PATH
-loads another build of libqsmd.so.
+on stderr; QSMD_BENCH_THREADS=1 prints the CPU time each thread of the
+process spent inside the window (/proc schedstat); QSMD_BENCH_PIN=1 pins the
+main thread to one core after the warm-up (the threads RCCL created keep
+the process's cores); QSMD_BENCH_DEVICE=d pins every rank to GPU d;
+QSMD_LIB_PATH loads another build of libqsmd.so.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
@@ -38,6 +41,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 # HIP reads GPU_MAX_HW_QUEUES when it initialises (the first torch CUDA call):
@@ -87,6 +91,20 @@ def alg_bytes(hdr, nodes):
 def hbm_bytes(hdr):
     """Bytes that must cross HBM: header + events in, status + nodes out."""
     return int((16 + 8 * hdr["n_ev"].astype(np.int64) + 1 + 8).sum())
+
+
+def thread_cpu_ns():
+    """{thread id: (name, ns on a CPU)} of this process (/proc schedstat)."""
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/comm") as f:
+                name = f.read().strip()
+            with open(f"/proc/self/task/{tid}/schedstat") as f:
+                out[int(tid)] = (name, int(f.read().split()[0]))
+        except (OSError, ValueError, IndexError):
+            pass
+    return out
 
 
 def host_cores():
@@ -204,6 +222,10 @@ class InFlight:
         self.ctxs[0].timing_reset()
         for c in self.ctxs:
             c.set_param("timing_events", self.timing_events)
+        if os.environ.get("QSMD_BENCH_PIN") == "1":     # (diagnostic, DESIGN.md §9: the main thread alone on a core)
+            os.sched_setaffinity(0, {min(os.sched_getaffinity(0))})
+        threads = os.environ.get("QSMD_BENCH_THREADS") == "1"
+        th0 = thread_cpu_ns() if threads else None
         self.steps_run = 0
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -223,6 +245,12 @@ class InFlight:
         # DESIGN.md §9)
         t_end = time.perf_counter()
         elapsed = t_end - t0
+        if threads:                            # each thread's CPU time inside the window
+            th1 = thread_cpu_ns()
+            busy = {f"{th1[t][0]}:{t}": round((th1[t][1] - th0.get(t, ("", 0))[1]) * 1e-6, 3) for t in th1}
+            print(json.dumps({"window_ms": round(elapsed * 1e3, 3), "main_tid": threading.get_native_id(),
+                              "thread_cpu_ms": {k: v for k, v in sorted(busy.items(), key=lambda kv: -kv[1]) if v > 0}}),
+                  file=sys.stderr)
         if os.environ.get("QSMD_BENCH_HOSTTIME") == "1":   # where the window's host time goes
             print(json.dumps({"enqueue_ms": (t_drain - t0) * 1e3, "sum_ms": (t_sync - t_drain) * 1e3,
                               "sync_ms": (t_end - t_sync) * 1e3}), file=sys.stderr)

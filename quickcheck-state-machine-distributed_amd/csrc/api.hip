@@ -112,7 +112,12 @@ struct qsmd_ctx {
     uint32_t* probe_host = nullptr;    // pinned: [defer, heavy32, heavy64, giant, timed] of the last finished call
     uint32_t* debug_host = nullptr;    // QSMD_SYNC_STAGES: giant-stage heartbeat (pinned)
     // lane mode's tables: one per lane slot of the memo grid
-    uint64_t memo_grid = 0;            // heavy stage (lane mode): workgroups at most (0 = 12 per CU); one table each
+    // heavy stage (lane mode): workgroups at most (0 = 32 per CU, so a long
+    // heavy list gets one workgroup per group of 64 histories and the
+    // dispatcher starts each group as soon as a slot frees: config 3's heavy
+    // stage alone 1.34 -> 1.09 ms against 12 per CU with grid-stride groups,
+    // tools/gpu/r06_c3sweep.sh); one table each
+    uint64_t memo_grid = 0;
     uint64_t mt_entries = 128;
     uint64_t memo_after = 32;          // lane mode: the memo joins a search after this many nodes
     // lane mode: stage 0's saved search states (80 B each), slots per heavy-
@@ -418,7 +423,7 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->dag_states = value;
     } else if (n == "dag_debug_ptr") {      // diagnostic: device buffer (16 + DAG LDS words) for one history
         c->dag_dbg = reinterpret_cast<uint32_t*>(value);
-    } else if (n == "stage0_stamps_ptr") {  // diagnostic build (QSMD_DIAG_STAGE0=2): 8 x u64 per workgroup
+    } else if (n == "stage0_stamps_ptr") {  // diagnostic build (tools/diag/compact_diag.patch, QSMD_DIAG_STAGE0=2): 8 x u64 per workgroup
         c->s0_stamps = reinterpret_cast<unsigned long long*>(value);
     } else if (n == "dag_debug_hist") {
         c->dag_dbg_h = value;
@@ -455,7 +460,7 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
     } else if (n == "wave_max") {
         c->wave_max = value;
     } else if (n == "memo_grid") {
-        if (value > 65536) return fail(c, QSMD_ERR_ARG, "memo_grid in 0..65536 (0 = 12 per CU)");
+        if (value > 65536) return fail(c, QSMD_ERR_ARG, "memo_grid in 0..65536 (0 = 32 per CU)");
         if (value != c->memo_grid && c->mt) {
             quiesce(c);
             (void)hipFree(c->mt);
@@ -644,7 +649,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // twice the groups expected -- they would hold CUs the next call's
     // stage 0 could use)
     const uint64_t mg = lt && !wide ? std::min<uint64_t>(c->n_cu, 2 * std::min<uint64_t>(g32, c->n_cu) + 8)
-                                    : (c->probe_valid ? tail_grid(8, c->memo_grid ? c->memo_grid : 12ull * c->n_cu,
+                                    : (c->probe_valid ? tail_grid(8, c->memo_grid ? c->memo_grid : 32ull * c->n_cu,
                                                                   heavy_hint + heavy_hint / 4)
                                                       : (uint64_t)c->n_cu);   // (no hint: grid-stride)
     if (lane && !(lt && !wide)) lane = lane_tables(c, s, mg);

@@ -31,17 +31,9 @@
 #include "internal.h"
 #include "lane.h"
 
-// Diagnostic builds only (tools/build_variant.sh): QSMD_DIAG_STAGE0=1 runs
-// stage 0 without the search (staging, masks and I/O alone); =2 runs it
-// whole and stamps each group's phases (a.stamps, tools/stage0_anatomy.py).
-#ifndef QSMD_DIAG_STAGE0
-#define QSMD_DIAG_STAGE0 0
-#endif
-// QSMD_DIAG_NOHEAVY=1: no heavy-list append (the budget-stopped histories
-// are reported BUDGET), to price the append
-#ifndef QSMD_DIAG_NOHEAVY
-#define QSMD_DIAG_NOHEAVY 0
-#endif
+// (Diagnostic builds -- stage 0 without its search, per-group phase stamps,
+// no heavy-list append -- are a patch applied to a copy of this file by
+// tools/build_variant.sh: tools/diag/compact_diag.patch.)
 
 namespace qsmd {
 
@@ -73,20 +65,6 @@ __device__ __forceinline__ int run_search(DFS& dfs, const SearchArgs& a, const u
     }
     return dfs.finish(status);
 }
-
-#if QSMD_DIAG_STAGE0 == 2
-template <class DFS>
-__device__ __forceinline__ int run_search_counted(DFS& dfs, const SearchArgs& a, const uint32_t* evc,
-                                                  int32_t (*s_bal)[C_LANES], int lane, uint64_t limit,
-                                                  uint32_t& iter) {
-    int status;
-    do {
-        status = dfs.template step<C_LANES>(a, evc, s_bal, lane, limit);
-        ++iter;
-    } while (status < 0);
-    return dfs.finish(status);
-}
-#endif
 
 // Stage the histories of the `fresh` lanes (history h) into their LDS
 // columns and classify them: returns -2 (deferred to the next stage), -1
@@ -148,9 +126,6 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
     const uint64_t user_limit = a.max_nodes ? a.max_nodes : ~0ull;
     const bool tiered = a.stage0_budget < user_limit && a.heavy_list != nullptr;
     const uint64_t limit = tiered ? a.stage0_budget : user_limit;
-#if QSMD_DIAG_STAGE0 == 2
-    const uint64_t rt_entry = __builtin_amdgcn_s_memrealtime();
-#endif
 
     // groups of 64 histories, grid-stride
     for (uint64_t base = (uint64_t)blockIdx.x * C_LANES; base < total; base += (uint64_t)gridDim.x * C_LANES) {
@@ -159,40 +134,14 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
         const uint32_t h = active ? (a.list ? a.list[idx] : (uint32_t)idx) : 0u;
         qsmd_hdr H;
         LaneDFS<MODEL, G> dfs;
-#if QSMD_DIAG_STAGE0 == 2
-        const uint64_t ts0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
         int status = stage_fresh<MODEL, G>(a, active, h, s_ev, s_bal, lane, dfs, H);
         const bool live = status != -2;     // (-2: no history here, or handed to the next stage)
-#if QSMD_DIAG_STAGE0 == 1
-        if (status == -1) status = QSMD_STATUS_LINEARISABLE;   // diagnostic build: no search
-#endif
         const bool search = status == -1;
         const uint32_t n_ev = H.n_ev;
-#if QSMD_DIAG_STAGE0 == 2
-        {   // stamps of the group: s_memtime at its start / after staging / after the search,
-            // s_memrealtime at the start / after the search / at the workgroup's entry, DFS iterations
-            const uint64_t ts1 = __builtin_amdgcn_s_memtime();
-            uint32_t it = 0;
-            if (search) status = run_search_counted(dfs, a, &s_ev[0][lane], s_bal, lane, limit, it);
-            for (int off = 32; off > 0; off >>= 1) it = max(it, (uint32_t)__shfl_xor((int)it, off, 64));
-            const uint64_t ts2 = __builtin_amdgcn_s_memtime(), rt2 = __builtin_amdgcn_s_memrealtime();
-            const uint64_t g = base / C_LANES;
-            if (a.stamps && lane < 7) {
-                const uint64_t v = lane == 0 ? ts0 : lane == 1 ? ts1 : lane == 2 ? ts2 : lane == 3 ? rt0
-                                 : lane == 4 ? rt2 : lane == 5 ? (uint64_t)it : rt_entry;
-                a.stamps[g * 8 + lane] = v;
-            }
-        }
-#else
         // the general path (pid masks): finish_lane does not pair (lane.h)
         if (search) status = run_search(dfs, a, &s_ev[0][lane], s_bal, lane, limit, h, t0);
-#endif
         note_failure(a, h, status);
         // over the stage budget (not the caller's): searched again by the heavy stage
-#if QSMD_DIAG_NOHEAVY
-        const bool heavy = false;   // diagnostic build: budget-stopped histories are reported BUDGET (no list)
-#else
         const bool heavy = tiered && status == QSMD_STATUS_BUDGET && dfs.nodes >= limit;
         if (a.heavy_shard_cap) {    // (stage 0: the group's shard, internal.h)
             const uint32_t k = (uint32_t)((base / C_LANES) % kShards);
@@ -205,7 +154,6 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
         } else {
             wave_append(heavy, h, a.heavy_list, a.heavy_count, lane);
         }
-#endif
         const bool out = live && !heavy;
         if (out) {
             a.status[h] = (uint8_t)status;
@@ -215,10 +163,6 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
         cnt.add(out, status, dfs.nodes);    // (every lane: the status counts are ballots)
     }
     cnt.flush(a.buckets, lane);
-#if QSMD_DIAG_STAGE0 == 2
-    if (a.stamps && lane == 7 && (uint64_t)blockIdx.x * C_LANES < total)   // the workgroup's exit
-        a.stamps[(uint64_t)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
-#endif
 }
 
 

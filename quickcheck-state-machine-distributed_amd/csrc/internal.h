@@ -160,9 +160,9 @@ struct SearchArgs {
     // histories a stage hands on to the giant stage (split search)
     uint32_t* giant_list;
     uint32_t* giant_count;
-    // diagnostic build only (QSMD_DIAG_STAGE0=2, stage0_stamps_ptr): stage 0
-    // writes 8 x u64 per group (compact.hip: phase stamps, DFS iterations,
-    // the workgroup's entry and exit)
+    // diagnostic build only (tools/diag/compact_diag.patch with
+    // QSMD_DIAG_STAGE0=2, stage0_stamps_ptr): stage 0 writes 8 x u64 per
+    // group (phase stamps, DFS iterations, the workgroup's entry and exit)
     unsigned long long* stamps;
 };
 
