@@ -707,6 +707,7 @@ def main():
     # one included).  Beside them: the same stage-0 bytes per step of the
     # timed region, and what the PMC counters of a profiled run of the same
     # configuration and budget give for the same launches.
+    # (budget_used 0xFFFFFFFF: stage 0 ran without a budget -- no heavy stage)
     heavy = nd0.astype(np.int64) > budget_used
     n_ev0 = hdr["n_ev"].astype(np.int64)
     kern = {"stage0": {"kernel": "compact_search<Bank, G32> (stage 0)", "ms": roof_s0,

@@ -748,7 +748,10 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     p.early = early ? 1u : 0u;
     p.totals = tot;
     p.probe_host = c->probe_host;
-    p.probe_budget = (uint32_t)std::min<uint64_t>(budget0, 0xFFFFFFFFull);
+    // the budget stage 0 runs with (a0.stage0_budget below: capped below
+    // 2^31), 0xFFFFFFFF when it has none (budget 0: stage 0 searches every
+    // history to its end) -- qsmd_get_param("stage0_budget_last")
+    p.probe_budget = budget0 ? (uint32_t)std::min<uint64_t>(budget0, 0x7FFFFFFFull) : 0xFFFFFFFFu;
     p.stall_ticks = c->giant_stall_us * 100ull;   // 100 MHz s_memrealtime
     if (flags & QSMD_FLAG_MEMO) {
         rc = memo_prepare(c, s, &p.memo, &p.memo_epoch);
@@ -1154,6 +1157,7 @@ int qsmd_get_param(qsmd_ctx* c, const char* name, uint64_t* out) {
     std::lock_guard<std::mutex> g(c->mu);
     const std::string n(name);
     if (n == "stage0_budget_last") {         // the stage-0 budget of the most recent finished call
+                                             // (0xFFFFFFFF: none, stage 0 searched every history to its end)
         quiesce(c);
         if (!__atomic_load_n(&c->probe_host[kProbeWritten], __ATOMIC_ACQUIRE))
             return fail(c, QSMD_ERR_ARG, "stage0_budget_last: no finished check call");

@@ -1,8 +1,9 @@
-// split.h -- the giant stage's device code (included by split.hip, whose
-// kernels launch it, and by memo.hip, whose folded lane-mode tail runs it
-// when a call has giants but no giant launch): every history the compact and
-// heavy stages hand on (beyond their geometry, or over their work caps),
-// searched by one lane or split over many; then the totals.
+// split.h -- the giant stage's device code (included by split.hip only, whose
+// kernels launch it; with lane mode's folded tail, api.hip `fold`, stage 0's
+// deferred histories reach it straight from the heavy stage's forward list):
+// every history the compact and heavy stages hand on (beyond their geometry,
+// or over their work caps), searched by one lane or split over many
+// (SURVEY.md §8e); then the totals.
 //
 // One launch per call (giant_search), phases chained inside it by counters:
 //

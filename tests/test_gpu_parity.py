@@ -919,3 +919,21 @@ def test_packed_lookalike_layouts(ctx):
     mixed = codec.encode(models.BANK, hs)
     assert len(mixed.events) == 32 * len(mixed.hdr)
     _compare(ctx, models.MODEL_BANK, mixed.hdr, mixed.events, max_nodes=10**7)
+
+
+def test_stage0_budget_last():
+    """qsmd_get_param("stage0_budget_last"): the budget stage 0 ran with --
+    the set one, capped below 2^31 (a saved state keeps its count in 32
+    bits), 0xFFFFFFFF for none (budget 0) -- which bench.py's roofline uses
+    to split stage 0's and the heavy stage's bytes."""
+    c = device.Context(0)
+    try:
+        hdr, ev, _ = gen.generate_config("bank_4x16_bugs", 3, 3000)
+        st_o, nd_o, _ = oracle_c.check_batch(models.MODEL_BANK, hdr, ev, threads=8)
+        for budget, want in ((20, 20), (0, 0xFFFFFFFF), ((1 << 31) + 5, 0x7FFFFFFF)):
+            c.set_stage0_budget(budget)
+            st, nd, _, _ = c.check_arrays(models.MODEL_BANK, hdr, ev)
+            assert c.get_param("stage0_budget_last") == want, budget
+            assert (st == st_o).all() and (nd == nd_o).all()
+    finally:
+        c.close()
