@@ -79,30 +79,45 @@ __device__ __forceinline__ bool keys_fit(const SearchArgs& a) {
     return ok;
 }
 
-// the key of the lane's current state (the node at depth dfs.depth); the
-// caller has checked keys_fit
+// The key of the lane's current state (the node at depth dfs.depth) in two
+// parts: the model's raw words (Bank: the eight balances, read from LDS; an
+// absent account holds 0 there -- LaneDFS: created from 0, restored to 0 by
+// undo -- so they are read unconditionally), then the key and its slot.
+// The caller has checked keys_fit.
+template <uint32_t MODEL>
+struct KeyRaw {
+    uint32_t b[MODEL == QSMD_MODEL_BANK ? QSMD_BANK_MAX_ACCOUNTS : 1];
+};
+
 template <uint32_t MODEL, class G>
-__device__ __forceinline__ LaneKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d, const SearchArgs& a,
-                                                      int32_t (*s_bal)[C_LANES], int lane, uint32_t epoch,
-                                                      SlotHash sh) {
-    LaneKey<MODEL, G> k;
-    k.rem_lo = (uint32_t)d.rem;
-    k.rem_hi = G::EV == 64 ? (uint32_t)((uint64_t)d.rem >> 32) : 0u;
-    uint32_t ex = 0;
+__device__ __forceinline__ KeyRaw<MODEL> memo_key_raw(int32_t (*s_bal)[C_LANES], int lane) {
+    KeyRaw<MODEL> r;
     if constexpr (MODEL == QSMD_MODEL_BANK) {
-        ex = d.ex;
-        // an absent account holds 0 in LDS (LaneDFS: created from 0, restored
-        // to 0 by undo), so the balances are read unconditionally; two i16
-        // halves per word by one v_perm
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            k.m[q] = __builtin_amdgcn_perm((uint32_t)s_bal[2 * q + 1][lane], (uint32_t)s_bal[2 * q][lane],
-                                           0x05040100u);
+        for (int q = 0; q < QSMD_BANK_MAX_ACCOUNTS; ++q) r.b[q] = (uint32_t)s_bal[q][lane];
+    } else {
+        r.b[0] = 0u;
+    }
+    return r;
+}
+
+template <uint32_t MODEL, class G>
+__device__ __forceinline__ LaneKey<MODEL, G> memo_key_of(const KeyRaw<MODEL>& r, typename G::M rem, uint32_t ex,
+                                                         uint32_t RS, uint32_t depth, const SearchArgs& a,
+                                                         uint32_t epoch, SlotHash sh) {
+    LaneKey<MODEL, G> k;
+    k.rem_lo = (uint32_t)rem;
+    k.rem_hi = G::EV == 64 ? (uint32_t)((uint64_t)rem >> 32) : 0u;
+    if constexpr (MODEL == QSMD_MODEL_BANK) {
+        // two i16 halves per word by one v_perm
+#pragma unroll
+        for (int q = 0; q < 4; ++q) k.m[q] = __builtin_amdgcn_perm(r.b[2 * q + 1], r.b[2 * q], 0x05040100u);
     } else {
         // model after the levels 0 .. depth-1 (the formula of LaneDFS::try_next)
-        const uint32_t just = d.RS ? 1u : a.m0_just;
-        const int32_t n = d.RS ? (int32_t)(d.depth - 1u - (31u - __builtin_clz(d.RS | 1u)))
-                               : (int32_t)a.m0_val[0] + (a.m0_just ? (int32_t)d.depth : 0);
+        ex = 0u;
+        const uint32_t just = RS ? 1u : a.m0_just;
+        const int32_t n = RS ? (int32_t)(depth - 1u - (31u - __builtin_clz(RS | 1u)))
+                             : (int32_t)a.m0_val[0] + (a.m0_just ? (int32_t)depth : 0);
         k.m[0] = just | (just ? ((uint32_t)n & 0xFFFFu) << 1 : 0u);
         k.m[1] = k.m[2] = k.m[3] = 0u;
     }
@@ -115,6 +130,13 @@ __device__ __forceinline__ LaneKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d
     if constexpr (G::EV == 64) t ^= __builtin_amdgcn_alignbit(k.rem_hi, k.rem_hi, 7);
     k.slot = (t * 0x9E3779B1u) >> sh.sh;
     return k;
+}
+
+template <uint32_t MODEL, class G>
+__device__ __forceinline__ LaneKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d, const SearchArgs& a,
+                                                      int32_t (*s_bal)[C_LANES], int lane, uint32_t epoch,
+                                                      SlotHash sh) {
+    return memo_key_of<MODEL, G>(memo_key_raw<MODEL, G>(s_bal, lane), d.rem, d.ex, d.RS, d.depth, a, epoch, sh);
 }
 
 template <uint32_t MODEL, class G>
@@ -229,18 +251,20 @@ struct PhaseClock {
 
 // One DFS iteration with the memo (LaneDFS::step plus the two hooks).
 // entry: the lane's column of node counts at entry, per level; tab: the
-// lane's HBM table, or (LT) its LDS column.
+// lane's HBM table, or (LT) its LDS column.  keyed: every reachable state
+// has a key (keys_fit), so a failed subtree is recorded from the heavy
+// stage's start; memo (the search has counted memo_after nodes): probes.
 template <uint32_t MODEL, class G, bool LT, bool ST>
 __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs& a, const uint32_t* evc,
                                          int32_t (*s_bal)[C_LANES], int lane, uint64_t limit, uint32_t* tab,
                                          uint32_t h, uint32_t epoch, SlotHash sh, uint32_t* entry, bool& skip,
-                                         uint64_t memo_after, Written& wr, PhaseClock* ph) {
+                                         bool keyed, uint64_t memo_after, Written& wr, PhaseClock* ph) {
     using M = typename G::M;
     // a short search runs as the plain DFS (no HBM probe per node); the memo
-    // joins once the search has counted memo_after nodes (entry counts are
-    // kept from the start, so a node entered before that is still recorded
-    // when it fails)
-    const bool memo = d.nodes >= memo_after;
+    // joins once the search has counted memo_after nodes.  Failed subtrees
+    // are recorded from the start (entry counts are kept from the start): a
+    // node that fails before the memo joins is found by the probes after.
+    const bool memo = keyed & (d.nodes >= memo_after);
     const bool empty = d.cand == (M)0;
     const bool term = empty & ((d.found == 0u) | (d.depth == d.base));
     int status = !term ? -1
@@ -252,27 +276,35 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     }
     if (empty & !term) {
         if constexpr (ST) t0 = ph->start();
-        // leaving the node at depth d.depth: its subtree was searched to the end and failed
-        // (counts kept mod 2^32: exact while the running count is below 2^32)
-        // (the level's entry count and the key's balances read together:
-        // gating the key on the entry count put its LDS round trip first)
-        const uint32_t ent = entry[(d.depth - 1u) * C_LANES];
-        if (memo && !skip && d.nodes <= 0xFFFFFFFFull) {
-            const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, sh);
-            const uint32_t cnt = (uint32_t)d.nodes - ent;
-            if (ent != kNoEntry) {
-                if constexpr (LT) {
-                    memo_insert_lds<MODEL, G>(tab, k, h, cnt);
-                } else {
-                    memo_insert<MODEL, G>(tab, k, h, cnt);
-                    wr.set(k.slot);
-                }
-            }
-        }
-        skip = false;
+        // leaving the node at depth d.depth: its subtree was searched to the
+        // end and failed (counts kept mod 2^32: exact while the running count
+        // is below 2^32).  The key (the node's balances, before the undo),
+        // the level's entry count and the undo's first read are issued
+        // together: one LDS round trip instead of three in a row
+        uint32_t ent = entry[(d.depth - 1u) * C_LANES];
+        KeyRaw<MODEL> raw = memo_key_raw<MODEL, G>(s_bal, lane);
+        const M rem0 = d.rem;
+        const uint32_t ex0 = d.ex, RS0 = d.RS, dep0 = d.depth;
         const uint32_t j = d.template undo<C_LANES>(evc, s_bal, lane);
+        // (the key's reads complete here, not sunk into the branch below: the
+        // compiler issues them beside the undo's)
+        if constexpr (MODEL == QSMD_MODEL_BANK)
+            asm volatile("" : "+v"(ent), "+v"(raw.b[0]), "+v"(raw.b[1]), "+v"(raw.b[2]), "+v"(raw.b[3]),
+                         "+v"(raw.b[4]), "+v"(raw.b[5]), "+v"(raw.b[6]), "+v"(raw.b[7]));
+        const bool rec = keyed & !skip & (d.nodes <= 0xFFFFFFFFull) & (ent != kNoEntry);
+        const uint32_t cnt = (uint32_t)d.nodes - ent;
+        skip = false;
         d.cand = cands(d.rem, d.INV, d.RESP) & mask_above(j, (M)0);
         d.found = 1u;
+        if (rec) {
+            const LaneKey<MODEL, G> k = memo_key_of<MODEL, G>(raw, rem0, ex0, RS0, dep0, a, epoch, sh);
+            if constexpr (LT) {
+                memo_insert_lds<MODEL, G>(tab, k, h, cnt);
+            } else {
+                memo_insert<MODEL, G>(tab, k, h, cnt);
+                wr.set(k.slot);
+            }
+        }
         if constexpr (ST) ph->stop(0, t0, lane);
     }
     if (d.cand) {
@@ -348,7 +380,8 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
         sh.sh = 32u - (uint32_t)__builtin_ctz(p.entries);
     }
     // a call with a model0 some reachable state has no key for: no memo
-    const uint64_t memo_after = keys_fit<MODEL, G>(a) ? (uint64_t)p.memo_after : ~0ull;
+    const bool keyed = keys_fit<MODEL, G>(a);
+    const uint64_t memo_after = (uint64_t)p.memo_after;
     const uint64_t idx = base + lane;
     const bool active = idx < total;
     uint64_t r0 = 0, c0 = 0;
@@ -428,7 +461,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
                 if (status < 0) {
                     const bool was = skip;
                     status = memo_step<MODEL, G, LT, ST>(dfs, a, &L.ev[0][lane], L.bal, lane, limit, tab, h,
-                                                         p.epoch, sh, &L.entry[0][lane], skip, memo_after, wr, ph);
+                                                         p.epoch, sh, &L.entry[0][lane], skip, keyed, memo_after, wr, ph);
                     if constexpr (ST) {
                         hits += (!was && skip) ? 1u : 0u;
                         ++lane_iter;

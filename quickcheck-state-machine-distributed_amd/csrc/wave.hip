@@ -852,6 +852,121 @@ __device__ int dag_history(const WaveArgs& p, const SearchArgs& a, const WaveDFS
                                                                    : QSMD_STATUS_NONLINEARISABLE);
 }
 
+// ---------------------------------------------------------------- chains
+// A TicketDispenser history whose state DAG is a chain: at every level the
+// candidates whose step is True all lead to one state (config 4's
+// adversarial 8 x 64 history on one shared pid: every pending TakeTicket is
+// a True candidate with the same successor -- filter1 and findResponse take
+// the pid's first remaining invocation and response whichever candidate is
+// tried -- so 64 levels of one state each).  A level is scalar work on the
+// event masks: a candidate's step depends only on its pid's first remaining
+// response (findResponse), its own request (TakeTicket / Reset) and the
+// uniform state (rem, Just n), so per pid the True candidates are the pid's
+// candidates among the TakeTickets or the Resets, whichever the response
+// answers (test/TicketDispenser.hs:99-102).  No LDS, no per-lane step, no
+// dedup table, no backward pass over LDS arrays.  Counts
+// (src/Linearisability.hs:59-69): along a chain, a state's False candidates
+// have no child and its True ones all enter the next state, so
+//   * a chain ending at a leaf (any' [] = True) is decided by each state's
+//     first True candidate: per state the candidates up to it;
+//   * a chain ending at a state whose candidates are all False fails
+//     everywhere: QSMD_FLAG_MEMO (each state's children once) counts every
+//     candidate of every state, the exhaustive DFS g(S) = deg(S) + nT(S) *
+//     g(next), folded from the bottom (past 2^64: BUDGET).
+// Returns -1 when the history is not such a chain (two True candidates of a
+// level with different successors): the DAG takes it from the root.
+template <typename M>
+__device__ int ticket_chain(const SearchArgs& a, const WaveDFS<QSMD_MODEL_TICKET, M>& d, uint32_t n_pid,
+                            bool memo_mode, uint64_t& nodes_out, uint32_t& path_len, uint32_t& pathv) {
+    constexpr uint32_t NW = Geo<M>::NW;
+    auto pid_ev = [&](uint32_t q) -> M {                // (uniform control flow: every lane active)
+        if constexpr (NW == 1) return __ballot(d.pidv[0] == q);
+        else return mk128(__ballot(d.pidv[0] == q), __ballot(d.pidv[1] == q));
+    };
+    const M ALL = d.INV | d.RESP;
+    // the TakeTicket requests (every other request of a valid history is a Reset)
+    M TT;
+    if constexpr (NW == 1) TT = __ballot(((d.lo[0] >> 8) & 0xFFu) == QSMD_TICKET_TAKE_TICKET) & d.INV;
+    else TT = mk128(__ballot(((d.lo[0] >> 8) & 0xFFu) == QSMD_TICKET_TAKE_TICKET),
+                    __ballot(((d.lo[1] >> 8) & 0xFFu) == QSMD_TICKET_TAKE_TICKET)) & d.INV;
+    const M RS = d.INV & ~TT;
+    M rem = ALL;
+    uint32_t just = a.m0_just;
+    int32_t n = (int32_t)a.m0_val[0];
+    uint64_t along = 0ull, items = 0ull;
+    uint32_t lvl = 0u, degv = 0u, ntv = 0u;
+    int status;
+    while (true) {
+        const M C = mcands(rem, d.INV, d.RESP);         // takeInvocations
+        // per pid: its first remaining response (findResponse) decides every
+        // candidate of the pid -- TakeTicket True iff it is Number (n + 1)
+        // under Just n, Reset True iff it is Ok (test/TicketDispenser.hs:99-102)
+        M IT{}, T{};
+        for (uint32_t q = 0; q < 8; ++q) {
+            if (q >= n_pid) break;
+            const M P = n_pid == 1u ? ALL : pid_ev(q);
+            const M rr = rem & P & d.RESP;
+            if (!mnz(rr)) continue;                     // no response: no child, not a node
+            const uint32_t rq = mctz(rr);
+            const uint32_t rc = (d.ev_lo(rq) >> 8) & 0xFFu;
+            const int32_t rv = d.ev_val(rq);
+            const M Cq = C & P;
+            IT |= Cq;
+            const bool ok_tt = rc == QSMD_TICKET_NUMBER && just != 0u && rv == n + 1;
+            const bool ok_rs = rc == QSMD_TICKET_OK;
+            T |= Cq & ((ok_tt ? TT : M{}) | (ok_rs ? RS : M{}));
+        }
+        const uint32_t deg = mpop(IT);
+        if (deg == 0u) {                                // any' [] = True; the root: any [] = False
+            status = lvl ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE;
+            break;
+        }
+        const uint32_t nt = mpop(T);
+        items += deg;
+        degv = wl(degv, deg, lvl);
+        ntv = wl(ntv, nt, lvl);
+        if (nt == 0u) {                                 // every candidate False: the chain fails
+            status = QSMD_STATUS_NONLINEARISABLE;
+            break;
+        }
+        // the first True candidate (the DFS's choice) and its successor: the
+        // pid's first remaining invocation and response gone (filter1,
+        // findResponse), TakeTicket succ <$>, Reset Just 0
+        // (test/TicketDispenser.hs:81-84).  Every True candidate must lead
+        // there: one pid, and one successor model
+        const uint32_t j = mctz(T);
+        along += mpop(IT & MaskOps<M>::below((int)j)) + 1u;
+        pathv = wl(pathv, j, lvl);
+        const M Pj = n_pid == 1u ? ALL : pid_ev(d.ev_lo(j) & 0x7Fu);
+        const bool tj = mnz(TT & mbit<M>(j));
+        if (mnz(T & ~Pj) || (mnz(T & TT) && mnz(T & RS) && n + 1 != 0)) return -1;   // two successors
+        rem &= ~(mlowest(rem & Pj & d.INV) | mlowest(rem & Pj & d.RESP));
+        n = tj ? n + 1 : 0;
+        just = 1u;
+        ++lvl;
+    }
+    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
+    uint64_t c = status == QSMD_STATUS_LINEARISABLE ? along : items;
+    bool sat = false;
+    if (status == QSMD_STATUS_NONLINEARISABLE && !memo_mode && lvl > 0u) {
+        // exhaustive: each True candidate searches the failing state below again
+        uint64_t g = rl(degv, lvl);
+        for (int k = (int)lvl - 1; k >= 0 && !sat; --k) {
+            uint64_t x;
+            sat = __builtin_mul_overflow((uint64_t)rl(ntv, (uint32_t)k), g, &x) ||
+                  __builtin_add_overflow(x, (uint64_t)rl(degv, (uint32_t)k), &g);
+        }
+        c = g;
+    }
+    path_len = status == QSMD_STATUS_LINEARISABLE ? lvl : 0u;
+    if (sat || c > limit) {
+        nodes_out = limit;
+        return QSMD_STATUS_BUDGET;
+    }
+    nodes_out = c;
+    return status;
+}
+
 __device__ __forceinline__ void clear_table(uint32_t* tab, uint32_t buckets, int lane) {
     // every word 0xFFFFFFFF (word 2 never matches), 16 B per lane and store
     uint4* t4 = reinterpret_cast<uint4*>(tab);
@@ -928,11 +1043,17 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
         status = QSMD_STATUS_SKIPPED;
     }
     const uint64_t c0 = p.stats ? __builtin_amdgcn_s_memtime() : 0ull;
-    if (status < 0 && dag_base) {                    // the state DAG, when it fits
+    if (status < 0 && dag_base) {                    // a chain, else the state DAG when it fits
         const DagLds L = dag_carve<MODEL, M>(dag_base, p.dag_states, p.dag_items);
         uint64_t dn = 0ull;
-        uint32_t plen = 0u;
-        const int ds = dag_history<MODEL, M>(p, a, d, n_ev, H.n_pid, L, p.dag_states, p.dag_items, lane, dn, plen);
+        uint32_t plen = 0u, pathv = 0u;
+        int ds = -1;
+        bool chain = false;
+        if constexpr (MODEL == QSMD_MODEL_TICKET) {
+            ds = ticket_chain<M>(a, d, H.n_pid, p.memo_mode != 0u, dn, plen, pathv);
+            chain = ds >= 0;
+        }
+        if (ds < 0) ds = dag_history<MODEL, M>(p, a, d, n_ev, H.n_pid, L, p.dag_states, p.dag_items, lane, dn, plen);
         if (ds >= 0) {
             if (p.stats && lane == 0) {
                 const unsigned long long cyc = __builtin_amdgcn_s_memtime() - c0;
@@ -959,8 +1080,13 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
             }
             if (a.witness && ds == QSMD_STATUS_LINEARISABLE) {
                 uint8_t* w = a.witness + H.ev_off;
-                for (uint32_t k = (uint32_t)lane; k <= plen && k < n_ev; k += 64u)
-                    w[k] = k < plen ? (uint8_t)L.path[k] : QSMD_WITNESS_END;
+                if (chain) {                         // (a chain of <= 64 levels: lane k holds level k's)
+                    if ((uint32_t)lane < plen) w[lane] = (uint8_t)pathv;
+                    if (lane == 0 && plen < n_ev) w[plen] = QSMD_WITNESS_END;
+                } else {
+                    for (uint32_t k = (uint32_t)lane; k <= plen && k < n_ev; k += 64u)
+                        w[k] = k < plen ? (uint8_t)L.path[k] : QSMD_WITNESS_END;
+                }
             }
             __syncthreads();                         // (L.path read before the next history reuses it)
             return;

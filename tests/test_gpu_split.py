@@ -336,3 +336,94 @@ def test_stalled_giant_workgroup_reports_budget(ctx):
     assert tot["budget"] == int(budget.sum())
     # the context is sound afterwards
     _compare(ctx, models.MODEL_TICKET, second[0], second[1], max_nodes=10**7)
+
+
+def _ticket_chain_like(rng, n_ops, width, n_pid, p_reset=0.1, p_bug=0.3):
+    """Config-4-shaped TicketDispenser histories: a Reset, then batches of up
+    to `width` pending invocations answered in order (responses numbered as a
+    sequential run would), over `n_pid` pids (1: the shared pid of
+    test/TicketDispenser.hs:302-309); sometimes a Reset among them or one
+    response off by one.  Most are chains of one state per level (the wave
+    stage's chain path); a Reset beside a TakeTicket gives two successors."""
+    pids = [f"p{i}" for i in range(n_pid)]
+    h = [("p0", ("L", "Reset")), ("p0", ("R", "Ok"))]
+    n, left = 0, n_ops - 1
+    while left > 0:
+        w = min(rng.randint(1, width), left)
+        ops = ["Reset" if rng.random() < p_reset else "TakeTicket" for _ in range(w)]
+        who = [pids[(k + rng.randint(0, n_pid - 1)) % n_pid] if n_pid > 1 else "p0" for k in range(w)]
+        h += [(who[k], ("L", ops[k])) for k in range(w)]
+        for k in range(w):
+            if ops[k] == "Reset":
+                h.append((who[k], ("R", "Ok")))
+                n = 0
+            else:
+                n += 1
+                h.append((who[k], ("R", ("Number", n))))
+        left -= w
+    if rng.random() < p_bug:
+        k = max(i for i, (_, ev) in enumerate(h) if ev[0] == "R")
+        if h[k][1][1] != "Ok":
+            h[k] = (h[k][0], ("R", ("Number", h[k][1][1][1] + 1)))
+    return h
+
+
+@pytest.mark.parametrize("bug", [0, 1])
+@pytest.mark.parametrize("nc,no", [(8, 64), (4, 17), (6, 30), (3, 10), (8, 40), (1, 9), (2, 64), (64, 64)])
+def test_ticket_chain_memo(ctx, nc, no, bug):
+    """The wave stage's chain path (wave.hip ticket_chain): adversarial
+    histories of several widths and lengths in QSMD_FLAG_MEMO mode --
+    verdict, explored count and witness equal to the oracle's memo mode."""
+    h, e, _ = gen.adversarial_ticket(nc, no, bug=bool(bug))
+    st_o, nd_o, w_o = oracle_c.check_batch(models.MODEL_TICKET, h, e, memo=True, witness=True)
+    st, nd, w, _ = ctx.check_arrays(models.MODEL_TICKET, h, e, flags=EXH | MEMO, witness=True)
+    assert (int(st[0]), int(nd[0])) == (int(st_o[0]), int(nd_o[0]))
+    if int(st[0]) == codec.STATUS_LIN:
+        assert np.array_equal(w, w_o)
+
+
+@pytest.mark.parametrize("nc,no", [(4, 17), (3, 10), (2, 30), (1, 40), (5, 12), (2, 40), (1, 60)])
+def test_ticket_chain_exhaustive(ctx, nc, no):
+    """The chain's exhaustive count g(S) = deg(S) + nT(S) g(next), against
+    the reference DFS's count (oracle, no memo)."""
+    for bug in (False, True):
+        h, e, _ = gen.adversarial_ticket(nc, no, bug=bug)
+        _compare(ctx, models.MODEL_TICKET, h, e, max_nodes=10**9)
+
+
+@pytest.mark.parametrize("memo", [False, True])
+@pytest.mark.parametrize("n_pid", [1, 2, 8])
+def test_ticket_chain_like_batches(ctx, n_pid, memo):
+    """Chain-shaped histories (and near-chains whose Reset makes two
+    successors: the DAG's) of 8..128 events through the host entry and the
+    heavy stage's wave mode, with node budgets and model0 variants."""
+    rng = random.Random(1000 + n_pid)
+    hs = [_ticket_chain_like(rng, rng.randint(4, 64), rng.randint(1, 8), n_pid) for _ in range(400)]
+    b = codec.encode(models.TICKET, hs)
+    flags = EXH | (MEMO if memo else 0)
+    ctx.set_param("heavy_mode", 0)
+    ctx.set_stage0_budget(2)
+    try:
+        # (exhaustive: budgets, since a wide chain's DFS count is (w!)^levels)
+        for max_nodes, m0 in ((10**5, None), (40, None), (10**5, models.TicketModel(1, 0, 3)),
+                              (10**5, models.TicketModel(0, 0, 0))):
+            if memo and max_nodes == 40:
+                continue
+            if memo:
+                max_nodes = 0
+            st, nd, w, _ = ctx.check_arrays(models.MODEL_TICKET, b.hdr, b.events, m0, flags=flags,
+                                            max_nodes=max_nodes, witness=True)
+            st_o, nd_o, w_o = oracle_c.check_batch(models.MODEL_TICKET, b.hdr, b.events, m0, max_nodes, 8,
+                                                   witness=True, memo=memo)
+            # (memo mode: the compact stages count the reference's nodes, the
+            # wave stage the pruning DFS's -- verdicts and witnesses compared)
+            diff = (st != st_o) if memo else ((st != st_o) | (nd != nd_o))
+            bad = np.nonzero(diff)[0]
+            assert len(bad) == 0, (max_nodes, bad[:5], st[bad[:5]], st_o[bad[:5]], nd[bad[:5]], nd_o[bad[:5]])
+            lin = np.nonzero(st == codec.STATUS_LIN)[0]
+            for i in lin:
+                a0, a1 = int(b.hdr[i]["ev_off"]), int(b.hdr[i]["ev_off"]) + int(b.hdr[i]["n_ev"])
+                assert np.array_equal(w[a0:a1], w_o[a0:a1]), i
+    finally:
+        ctx.set_param("heavy_mode", 2)
+        ctx.set_stage0_budget(32)

@@ -73,14 +73,14 @@ def rotr(x, k):
 
 
 def slot_of(rem, ex, bal, mask):
-    """memo.hip memo_key: the slot hash, or None when a balance is beyond i16."""
+    """memo.hip memo_key: the slot hash (the top bits of one multiplicative
+    hash), or None when a balance is beyond i16."""
     if any(not (-32768 <= v <= 32767) for v in bal):
         return None
     m = [((bal[2 * q] & 0xFFFF) | ((bal[2 * q + 1] & 0xFFFF) << 16)) & M32 for q in range(4)]
-    v = m[0] ^ rotr(m[1], 8) ^ rotr(m[2], 16) ^ rotr(m[3], 24)
-    h = ((rem * 0x9E3779B1) & M32) ^ ((ex * 0x85EBCA77) & M32) ^ ((v * 0xC2B2AE3D) & M32)
-    h ^= (h >> 16) ^ (h >> 24)
-    return h & mask
+    v = m[0] ^ ex ^ rotr(m[1], 8) ^ rotr(m[2], 16) ^ rotr(m[3], 24)
+    t = (rem & M32) ^ rotr(v, 13)
+    return ((t * 0x9E3779B1) & M32) >> (32 - (mask + 1).bit_length() + 1)
 
 
 class Hist:
@@ -109,7 +109,7 @@ def lowbit(x):
     return (x & -x).bit_length() - 1
 
 
-def run(h, budget, memo_after, entries):
+def run(h, budget, memo_after, entries, policy="backtrack", alias=64, record_early=False):
     """Returns (status, nodes, iterations after the resume, stage-0 iterations, descents, hits)."""
     ALL = h.INV | h.RESP
     rem, ex, bal = ALL, 0, (0,) * 8
@@ -119,6 +119,8 @@ def run(h, budget, memo_after, entries):
     found, nodes, depth = 0, 0, 0
     table = {}
     mask = entries - 1 if entries else 0
+    own = set()             # policy 'entry': alias classes of the path's pending slots
+    pslot = []              # policy 'entry': the level's pending slot (None: none)
     limit = budget
     phase0 = True
     it0 = it1 = desc = hits = 0
@@ -136,7 +138,11 @@ def run(h, budget, memo_after, entries):
         if term:
             return (1 if (not found and depth > 0) else 0), nodes, it1, it0, desc, hits
         if empty:
-            if memo and not skip and entry[depth - 1] is not None:
+            ps = pslot.pop()
+            if ps is not None:                  # policy 'entry': the pending entry gets its count
+                own.discard(ps % alias)
+                table[ps] = (table[ps][0], nodes - entry[depth - 1])
+            if policy == "backtrack" and (memo or (record_early and not phase0)) and not skip and entry[depth - 1] is not None:
                 cnt = nodes - entry[depth - 1]
                 key = (rem, ex, bal)
                 if entries:
@@ -165,6 +171,7 @@ def run(h, budget, memo_after, entries):
                 phase0 = False
                 limit = 1 << 62
                 entry = [None] * len(entry)
+                pslot = [None] * len(pslot)
                 info["depth"] = depth
                 info["cand"] = bin(cand).count("1")
                 info["stack_untried"] = sum(bin(cands(pr, h) & ~((2 << pj) - 1)).count("1") for pr, _, _, pj in stack)
@@ -182,19 +189,30 @@ def run(h, budget, memo_after, entries):
                 fi = rem & p & h.INV
                 stack.append((rem, ex, bal, j))
                 entry.append(nodes)
+                pslot.append(None)
                 ex, bal = bank_next(ex, bal, (h.code[j], h.a[j], h.b[j], h.val[j]))
                 rem = rem & ~((fi & -fi) | (1 << r))
                 depth += 1
                 desc += 1
                 cand = cands(rem, h)
                 found = 0
-                if memo:
+                if memo or (policy in ("entry", "noevict") and not phase0 and record_early):
                     key = (rem, ex, bal)
                     cnt = None
                     if entries:
                         s = slot_of(rem, ex, bal, mask)
-                        if s is not None and s in table and table[s][0] == key:
+                        free = s is not None and (policy == "backtrack" or s % alias not in own)
+                        if memo and free and s in table and table[s][0] == key:
                             cnt = table[s][1]
+                            assert cnt is not None
+                        if policy == "noevict" and free and cnt is None and s not in table:
+                            table[s] = (key, None)
+                            own.add(s % alias)
+                            pslot[-1] = s
+                        if policy == "entry" and free and cnt is None:
+                            table[s] = (key, None)
+                            own.add(s % alias)
+                            pslot[-1] = s
                     else:
                         cnt = table.get(key)
                     if cnt is not None:
@@ -210,8 +228,11 @@ def main():
     budget = int(sys.argv[2]) if len(sys.argv) > 2 else 18
     memo_after = int(sys.argv[3]) if len(sys.argv) > 3 else 32
     entries = int(sys.argv[4]) if len(sys.argv) > 4 else 128
+    policy = sys.argv[5] if len(sys.argv) > 5 else "backtrack"
+    alias = int(sys.argv[6]) if len(sys.argv) > 6 else 64
+    config = sys.argv[7] if len(sys.argv) > 7 else "bank_4x16"
     import oracle_c
-    hdr, ev, _ = gen.generate_config("bank_4x16", 0, n, threads=8)
+    hdr, ev, _ = gen.generate_config(config, 0, n, threads=8)
     st_o, nd_o, _ = oracle_c.check_batch(2, hdr, ev, threads=8)
     heavy = np.nonzero(nd_o > budget)[0]
     its, its0, descs = [], [], []
@@ -219,14 +240,14 @@ def main():
     for i in heavy:
         hd = hdr[i]
         h = Hist(ev[int(hd["ev_off"]): int(hd["ev_off"]) + int(hd["n_ev"])])
-        s, nd, it1, it0, desc, hits = run(h, budget, memo_after, entries)
+        s, nd, it1, it0, desc, hits = run(h, budget, memo_after, entries, policy, alias, os.environ.get("EARLY") == "1")
         if s != int(st_o[i]) or nd != int(nd_o[i]):
             bad += 1
         its.append(it1)
         its0.append(it0)
         descs.append(desc)
     its = np.array(its)
-    print(f"n={n} budget={budget} memo_after={memo_after} entries={entries}: heavy {len(heavy)} "
+    print(f"n={n} budget={budget} memo_after={memo_after} entries={entries} policy={policy} alias={alias}: heavy {len(heavy)} "
           f"({len(heavy) / n:.4f}), mismatches {bad}")
     q = np.percentile(its, [50, 90, 99, 99.9, 100])
     print("iterations after resume: mean %.1f p50 %d p90 %d p99 %d p99.9 %d max %d" % (its.mean(), *q))
