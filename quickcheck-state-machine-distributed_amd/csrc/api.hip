@@ -884,12 +884,16 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         stage_done("wave", s, cnt);
     }
     {
-        // (2 per CU when the last call had giants; an early exit without
-        // them: one workgroup per fixup chunk, at least 8 and at most 2 per
-        // CU -- every workgroup of the launch takes the fixup's queue and
-        // exit atomics, 2 per CU made a 4096-history call's giant stage ~65 us)
+        // (2 per CU when the last call had giants, or when folded: stage 0's
+        // deferred histories, however many this call has, go straight to the
+        // giant stage -- the short path of a call without giants costs the
+        // same on 64 or 512 workgroups, profiles/r06/c3c4/giant_grid_split_budget.txt; an
+        // early exit without them: one workgroup per fixup chunk, at least 8
+        // and at most 2 per CU -- every workgroup of the launch takes the
+        // fixup's queue and exit atomics, 2 per CU made a 4096-history call's
+        // giant stage ~65 us)
         const uint64_t gg = c->giant_grid ? c->giant_grid
-                          : (hint[3] ? 2ull * c->n_cu
+                          : (hint[3] || (fold && !early) ? 2ull * c->n_cu
                                      : (early ? std::min<uint64_t>(2ull * c->n_cu,
                                                                    std::max<uint64_t>(8, (n_hist + kFixupChunk - 1) / kFixupChunk))
                                               : 64ull));
