@@ -967,6 +967,98 @@ __device__ int ticket_chain(const SearchArgs& a, const WaveDFS<QSMD_MODEL_TICKET
     return status;
 }
 
+// The chain of a history on ONE pid (the reference's own TicketDispenser
+// histories: every event on the test process's pid, test/TicketDispenser.hs:
+// 302-309), level-parallel.  With one pid, level k's state has lost the
+// first k invocations and the first k responses whichever candidates were
+// tried (filter1 / findResponse), so its candidates are the invocations of
+// rank >= k before the k-th response, and that response decides them all:
+// Number v makes exactly the TakeTickets True (when v = n_k + 1 under Just
+// n_k), Ok exactly the Resets (test/TicketDispenser.hs:99-102).  Every True
+// candidate enters the same state, so the DAG is always a chain, and the
+// model at level k > 0 is Just v or Just 0 from response k-1 (:81-84).
+// Lane k evaluates level k at once; the first level without a True
+// candidate or without candidates ends the chain, and the counts are
+// ticket_chain's (below).  scratch: >= 256 words of the wavefront's LDS.
+template <typename M>
+__device__ int ticket_shared_chain(const SearchArgs& a, const WaveDFS<QSMD_MODEL_TICKET, M>& d, uint32_t n_ev,
+                                   bool memo_mode, uint32_t* scratch, int lane, uint64_t& nodes_out,
+                                   uint32_t& path_len, uint32_t& pathv) {
+    constexpr uint32_t NW = Geo<M>::NW;
+    const uint32_t ul = (uint32_t)lane;
+    M TT;
+    if constexpr (NW == 1) TT = __ballot(((d.lo[0] >> 8) & 0xFFu) == QSMD_TICKET_TAKE_TICKET) & d.INV;
+    else TT = mk128(__ballot(((d.lo[0] >> 8) & 0xFFu) == QSMD_TICKET_TAKE_TICKET),
+                    __ballot(((d.lo[1] >> 8) & 0xFFu) == QSMD_TICKET_TAKE_TICKET)) & d.INV;
+    const M RS = d.INV & ~TT;
+    // the k-th invocation's position, the k-th response's position, code and
+    // value, by rank (event lanes scatter them into LDS)
+    uint32_t* inv_at = scratch;
+    uint32_t* resp_at = scratch + 64;
+    uint32_t* resp_code = scratch + 128;
+    int32_t* resp_val = reinterpret_cast<int32_t*>(scratch + 192);
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) {
+        const uint32_t e = ul + 64u * w;
+        const M below = MaskOps<M>::below((int)e);
+        const bool inv = e < n_ev && mnz(d.INV & mbit<M>(e)), resp = e < n_ev && mnz(d.RESP & mbit<M>(e));
+        const uint32_t ri = mpop(d.INV & below), rr = mpop(d.RESP & below);
+        if (inv && ri < 64u) inv_at[ri] = e;
+        if (resp && rr < 64u) {
+            resp_at[rr] = e;
+            resp_code[rr] = (d.lo[w] >> 8) & 0xFFu;
+            resp_val[rr] = d.val[w];
+        }
+    }
+    __syncthreads();
+    const uint32_t nI = mpop(d.INV), nR = mpop(d.RESP);
+    const uint32_t k = ul;
+    const bool hasR = k < nR;
+    const uint32_t I = k < nI ? inv_at[k] : 128u;
+    const uint32_t R = hasR ? resp_at[k] : 0u;
+    const uint32_t rc = hasR ? resp_code[k] : 0u;
+    const int32_t rv = hasR ? resp_val[k] : 0;
+    __syncthreads();                                    // (the scratch is free again)
+    // the model at level k: model0, then Just (response k-1's Number) or Just 0
+    const uint32_t prc = (uint32_t)__shfl((int)rc, (int)(k ? k - 1u : 0u), 64);
+    const int32_t prv = __shfl(rv, (int)(k ? k - 1u : 0u), 64);
+    const uint32_t just = k ? 1u : a.m0_just;
+    const int32_t n = k ? (prc == QSMD_TICKET_NUMBER ? prv : 0) : (int32_t)a.m0_val[0];
+    // candidates: invocations of rank >= k (positions >= I) before position R
+    const M W = hasR ? d.INV & ~MaskOps<M>::below((int)I) & MaskOps<M>::below((int)R) : M{};
+    const bool tt_ok = rc == QSMD_TICKET_NUMBER && just != 0u && rv == n + 1;
+    const M T = tt_ok ? W & TT : (rc == QSMD_TICKET_OK ? W & RS : M{});
+    const uint32_t deg = mpop(W), nt = mpop(T);
+    const uint32_t j = mnz(T) ? mctz(T) : 0u;
+    const uint32_t idx = mnz(T) ? mpop(W & MaskOps<M>::below((int)j)) : 0u;
+    const uint64_t stop = __ballot(deg == 0u || nt == 0u);
+    const uint32_t L = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;   // the chain's last level
+    const uint32_t degL = L < 64u ? rl(deg, L) : 0u;
+    int status = degL ? QSMD_STATUS_NONLINEARISABLE : (L ? QSMD_STATUS_LINEARISABLE : QSMD_STATUS_NONLINEARISABLE);
+    const uint64_t along = wave_sum64(k < L ? (uint64_t)idx + 1u : 0ull);
+    const uint64_t items = wave_sum64(k <= L ? (uint64_t)deg : 0ull);
+    pathv = j;
+    uint64_t c = status == QSMD_STATUS_LINEARISABLE ? along : items;
+    bool sat = false;
+    if (degL && !memo_mode && L > 0u) {                 // exhaustive: g = deg + nT g(next), from the bottom
+        uint64_t g = degL;
+        for (int q = (int)L - 1; q >= 0 && !sat; --q) {
+            uint64_t x;
+            sat = __builtin_mul_overflow((uint64_t)rl(nt, (uint32_t)q), g, &x) ||
+                  __builtin_add_overflow(x, (uint64_t)rl(deg, (uint32_t)q), &g);
+        }
+        c = g;
+    }
+    const uint64_t limit = a.max_nodes ? a.max_nodes : ~0ull;
+    path_len = status == QSMD_STATUS_LINEARISABLE ? L : 0u;
+    if (sat || c > limit) {
+        nodes_out = limit;
+        return QSMD_STATUS_BUDGET;
+    }
+    nodes_out = c;
+    return status;
+}
+
 __device__ __forceinline__ void clear_table(uint32_t* tab, uint32_t buckets, int lane) {
     // every word 0xFFFFFFFF (word 2 never matches), 16 B per lane and store
     uint4* t4 = reinterpret_cast<uint4*>(tab);
@@ -1050,7 +1142,8 @@ __device__ __forceinline__ void wave_history(const WaveArgs& p, uint32_t h, cons
         int ds = -1;
         bool chain = false;
         if constexpr (MODEL == QSMD_MODEL_TICKET) {
-            ds = ticket_chain<M>(a, d, H.n_pid, p.memo_mode != 0u, dn, plen, pathv);
+            ds = H.n_pid == 1u ? ticket_shared_chain<M>(a, d, n_ev, p.memo_mode != 0u, L.tab, lane, dn, plen, pathv)
+                               : ticket_chain<M>(a, d, H.n_pid, p.memo_mode != 0u, dn, plen, pathv);
             chain = ds >= 0;
         }
         if (ds < 0) ds = dag_history<MODEL, M>(p, a, d, n_ev, H.n_pid, L, p.dag_states, p.dag_items, lane, dn, plen);
