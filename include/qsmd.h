@@ -252,10 +252,18 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *   "dag_states"        wave mode: capacity in states of the per-wavefront
  *                       state DAG (default 128, items 4x that; 0 = the DFS
  *                       for every history); a history whose DAG does not fit
- *                       runs the DFS
- *   "memo_after"        lane mode: the memo joins a search after this many
- *                       nodes (default 32; before, the plain DFS without the
- *                       probe per node)
+ *                       runs the DFS.  A TicketDispenser history whose DAG is
+ *                       a chain (every history on one pid) runs as one
+ *                       (scalar mask work, no DAG arrays) unless it is 0
+ *   "memo_after"        lane mode: the memo probes a search's nodes after
+ *                       it counted this many (default 32; its failed
+ *                       subtrees are recorded from the start)
+ *   "tail_cap", "tail_min"  lane mode: a search still running after tail_cap
+ *                       wavefront iterations (default 256; 0 = never) goes to
+ *                       a wave-mode launch after the heavy stage and is
+ *                       searched there from the root (the state DAG), when
+ *                       the last finished call sent at least tail_min
+ *                       (default 65536) histories to the heavy stage
  *   "resume_cap"        lane mode: stage 0's saved search states, slots per
  *                       heavy-list shard (0 = automatic: twice the last
  *                       call's heavy count per shard, at least 1024); a heavy
@@ -268,7 +276,8 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *                       qsmd_last_kernel_ms); 0 (default until
  *                       qsmd_timing_reset): none
  *   "giant_grid"        giant stage workgroups (0 = 2 per CU, or 64 when the
- *                       last finished call had no giant history)
+ *                       last finished call had no giant history and lane
+ *                       mode's fold does not apply)
  *   "wave_stats_ptr", "memo_stats_ptr", "memo_stats_groups"  diagnostics:
  *                       device buffers: wave mode 16 x u64 (DFS iterations
  *                       max / sum, s_memtime cycles max / sum, nodes sum per
@@ -283,7 +292,7 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
 int qsmd_set_param(qsmd_ctx* ctx, const char* name, uint64_t value);
 
 /* Read a knob ("stage0_budget": 0 while automatic, "fold", "heavy_mode",
- * "memo_after", "resume_cap") or "stage0_budget_last": the stage-0 budget the most recent
+ * "memo_after", "resume_cap", "tail_cap", "tail_min") or "stage0_budget_last": the stage-0 budget the most recent
  * finished check call ran with (the automatic one included; waits for the
  * context's last call). */
 int qsmd_get_param(qsmd_ctx* ctx, const char* name, uint64_t* out);

@@ -120,6 +120,13 @@ struct qsmd_ctx {
     uint64_t memo_grid = 0;
     uint64_t mt_entries = 128;
     uint64_t memo_after = 32;          // lane mode: the memo joins a search after this many nodes
+    // lane mode's tail: a search still running after tail_cap wavefront
+    // iterations goes to a wave-mode launch after the heavy stage (one
+    // wavefront per history, the state DAG from the root), when the last
+    // call's heavy list had at least tail_min histories (a throughput-bound
+    // list whose longest searches set the stage's end); 0 = never
+    uint64_t tail_cap = 256;
+    uint64_t tail_min = 65536;
     // lane mode: stage 0's saved search states (80 B each), slots per heavy-
     // list shard: from the last call's heavy count (2x, at least 1024; an
     // eighth of the batch before the first call), or the knob resume_cap.  A
@@ -444,6 +451,10 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->timing = value != 0;
     } else if (n == "memo_after") {
         c->memo_after = value;
+    } else if (n == "tail_cap") {
+        c->tail_cap = value;
+    } else if (n == "tail_min") {
+        c->tail_min = value;
     } else if (n == "memo_lds_cap") {       // diagnostic: force the LDS-refused path (the HBM tables)
         c->memo_lds_cap = value;
     } else if (n == "memo_lds") {
@@ -601,6 +612,23 @@ static void giant_heartbeat(qsmd_ctx* c, hipStream_t s, uint64_t gg) {
 // goes straight to the wide list: one wave-mode launch and the giant stage)
 enum : uint32_t { kSkip0 = 1u, kSkip0w = 2u };
 
+// wave mode's launch arguments but the lists, the LDS table size and the
+// M128 launch (the heavy stage's wave mode and lane mode's tail launch)
+static WaveArgs wave_args(const qsmd_ctx* c, const SearchArgs& a, uint32_t flags, uint64_t cap, bool split) {
+    WaveArgs wp{};
+    wp.s = a;
+    wp.explore_cap = cap;
+    wp.explore_cap_wide = split ? 16 * c->split_budget : 0;   // (the giant stage's whole-search cap)
+    wp.stats = c->wave_stats;
+    wp.memo_min_rem = (uint32_t)c->wave_min_rem;
+    wp.dag_states = (uint32_t)(c->dag_states & ~1ull);   // (even: the DAG's LDS arrays stay 8-B aligned)
+    wp.dag_items = 4u * wp.dag_states;
+    wp.dbg = c->dag_dbg;
+    wp.dbg_h = (uint32_t)c->dag_dbg_h;
+    wp.memo_mode = (flags & QSMD_FLAG_MEMO) ? 1u : 0u;
+    return wp;
+}
+
 static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* hdr, uint64_t n_hist,
                                const qsmd_event* events, uint64_t n_events, const void* model0,
                                uint32_t flags, uint64_t max_nodes, uint8_t* status, uint64_t* nodes,
@@ -623,8 +651,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // block sets the probe's written flag)
     if (!c->probe_valid && c->any_call && __atomic_load_n(&c->probe_host[kProbeWritten], __ATOMIC_ACQUIRE))
         c->probe_valid = true;
-    uint32_t hint[9];
-    for (int i = 0; i < 9; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
+    uint32_t hint[kProbeSlots];
+    for (int i = 0; i < kProbeSlots; ++i) hint[i] = c->probe_valid ? c->probe_host[i] : 0xFFFFFFFFu;
     const uint64_t budget0 = stage0_budget_of(c, hint);
     // the automatic budget just went down: the last call's heavy count (at
     // the higher budget) undercounts this one's -- size the tail for a long
@@ -657,6 +685,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // to stage 0w and this one has a normal route -- no stage-0w launch
     const bool fold = lane && c->fold && c->probe_valid && route == 0u && !sync_stages() &&
                       hint[0] == 0u && hint[2] == 0u;
+    // lane mode's wave-mode tail launch (ctx.tail_cap): for a long heavy list
+    const bool tail = lane && c->tail_cap && c->probe_valid && heavy_hint >= c->tail_min && c->dag_states;
 
     // ---- workspace: header, lists, giant records, tasks
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
@@ -668,7 +698,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const size_t off_h64 = off_h32 + align_up(kShards * cap32 * 4 + 4);
     const size_t off_lw = off_h64 + lst;                 // stage 0w's deferred (wide) histories
     const size_t off_lg = off_lw + lst;                  // giants
-    const size_t off_gr = off_lg + lst;
+    const size_t off_lt = off_lg + lst;                  // lane mode -> the wave-mode tail launch
+    const size_t off_gr = off_lt + lst;
     const size_t off_tk = off_gr + align_up(n_hist * sizeof(GiantRec));
     const size_t off_ts = off_tk + align_up(n_tk * sizeof(qsmd_task));
     const size_t off_tn = off_ts + align_up(n_tk);
@@ -707,6 +738,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     uint32_t* h64 = reinterpret_cast<uint32_t*>(c->ws + off_h64);
     uint32_t* lw = reinterpret_cast<uint32_t*>(c->ws + off_lw);
     uint32_t* lg = reinterpret_cast<uint32_t*>(c->ws + off_lg);
+    uint32_t* lt_list = reinterpret_cast<uint32_t*>(c->ws + off_lt);
     if (early && !nodes) nodes = reinterpret_cast<uint64_t*>(c->ws + off_nd);
 
     a.hdr = hdr;
@@ -840,6 +872,9 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].lds_entries = lds_entries;
             mp[w].epoch = c->mt_epoch;
             mp[w].giant_cap = cap;
+            mp[w].tail_cap = tail ? c->tail_cap : 0u;
+            mp[w].tail_list = tail ? lt_list : nullptr;
+            mp[w].tail_count = cnt + C_TAIL;
             mp[w].stats = c->memo_stats;
             mp[w].stats_groups = c->memo_stats ? c->memo_stats_groups : 0;
             mp[w].fwd_list = lw;                 // stage 0w's deferred histories: on to the giant stage
@@ -848,9 +883,27 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         HIP_TRY(c, launch_memo(mp[0], mp[1], (uint32_t)mg, wide, lt, s, tm ? evs[3] : nullptr,
                                tm ? evs[4] : nullptr), "memo launch");
         stage_done("lane", s, cnt);
+        if (tail) {
+            // the tail: the lane-mode searches past tail_cap, one wavefront
+            // each (the list as wave mode's G32 list; the others empty)
+            WaveArgs wt = wave_args(c, a, flags, cap, split);
+            wt.list32 = lt_list;
+            wt.count32 = cnt + C_TAIL;
+            wt.cap32 = 0u;
+            wt.list64 = lt_list;
+            wt.count64 = cnt + C_ZERO;
+            wt.list_wide = lt_list;
+            wt.count_wide = cnt + C_ZERO;
+            wt.buckets = 32u;
+            wt.wide128 = 0u;
+            const uint64_t nt = hint[kProbeTail] == 0xFFFFFFFFu ? 4ull * c->n_cu : hint[kProbeTail];
+            const uint64_t gt = c->wave_grid ? c->wave_grid
+                                             : std::min<uint64_t>(16ull * c->n_cu, std::max<uint64_t>(64, nt + nt / 4));
+            HIP_TRY(c, launch_wave(wt, (uint32_t)gt, 0u, s), "tail launch");
+            stage_done("tail", s, cnt);
+        }
     } else {
-        WaveArgs wp{};
-        wp.s = a;
+        WaveArgs wp = wave_args(c, a, flags, cap, split);
         wp.list32 = h32;
         wp.count32 = shards;
         wp.cap32 = (uint32_t)cap32;
@@ -858,15 +911,6 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         wp.count64 = cnt + C_HEAVY64;
         wp.list_wide = (route & kSkip0w) ? nullptr : lw;
         wp.count_wide = cnt + C_WIDE;
-        wp.explore_cap = cap;
-        wp.explore_cap_wide = split ? 16 * c->split_budget : 0;   // (the giant stage's whole-search cap)
-        wp.stats = c->wave_stats;
-        wp.memo_min_rem = (uint32_t)c->wave_min_rem;
-        wp.dag_states = (uint32_t)(c->dag_states & ~1ull);   // (even: the DAG's LDS arrays stay 8-B aligned)
-        wp.dag_items = 4u * wp.dag_states;
-        wp.dbg = c->dag_dbg;
-        wp.dbg_h = (uint32_t)c->dag_dbg_h;
-        wp.memo_mode = (flags & QSMD_FLAG_MEMO) ? 1u : 0u;
         // LDS memo table: 8 KB per wavefront (256 entries of <= 64 events),
         // 64 KB when the last call had wide histories (1024 entries of <= 128)
         const uint64_t wide_hint = (route & kSkip0w) ? n_hist : (c->probe_valid ? (uint64_t)hint[kProbeWide] : 0ull);
@@ -1176,6 +1220,10 @@ int qsmd_get_param(qsmd_ctx* c, const char* name, uint64_t* out) {
         *out = c->heavy_mode;
     } else if (n == "memo_after") {
         *out = c->memo_after;
+    } else if (n == "tail_cap") {
+        *out = c->tail_cap;
+    } else if (n == "tail_min") {
+        *out = c->tail_min;
     } else {
         return fail(c, QSMD_ERR_ARG, "unknown parameter");
     }

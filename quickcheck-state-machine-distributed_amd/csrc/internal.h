@@ -61,6 +61,8 @@ enum Cnt : uint32_t {
     C_XDONE,            // fixup chunks finished
     C_EXIT,             // giant-stage blocks finished
     C_WIDE,             // stage 0w -> wave mode's wide list (or, in lane mode, on to the giant stage)
+    C_TAIL,             // lane mode -> the wave-mode tail launch (searches past tail_cap iterations)
+    C_ZERO,             // always 0 (the tail launch's empty lists)
     C_N = 32
 };
 
@@ -172,6 +174,8 @@ constexpr int kProbeWide = 5;
 constexpr int kProbeBudget = 6;   // the call's stage-0 budget and batch size (api.hip: the automatic budget)
 constexpr int kProbeN = 7;
 constexpr int kProbeWritten = 8;  // 1 once a call's giant stage wrote the probe (never reset)
+constexpr int kProbeTail = 9;     // the lane-mode searches handed to the wave-mode tail launch
+constexpr int kProbeSlots = 10;
 
 // Histories per early-exit fixup chunk of the giant stage (a workgroup takes
 // one at a time; a wavefront marks ~0.33 us per row of 64, so short chunks
@@ -181,6 +185,7 @@ constexpr uint32_t kFixupChunk = 512;
 
 // internal status: the search was handed to a later stage (not a result)
 constexpr int QSMD_STATUS_HANDED_OFF = 0x40;
+constexpr int QSMD_STATUS_TO_TAIL = 0x41;     // lane mode: on to the wave-mode tail launch (internal)
 
 // ------------------------------------------------------------ giant stage
 // One history searched by many lanes.  The frontier phase
@@ -318,6 +323,9 @@ struct MemoArgs {
     uint32_t lds_entries;         // LDS tables (lds_tables): entries per lane, a power of two <= 64
     uint32_t epoch;               // this call's tag (24 bits)
     uint64_t giant_cap;           // > 0: a search past this many iterations goes to s.giant_list
+    uint64_t tail_cap;            // > 0: a search past this many iterations goes to tail_list (wave mode)
+    uint32_t* tail_list;
+    uint32_t* tail_count;
     unsigned long long* stats;    // diagnostic (memo_stats_ptr): 8 x u64 per group of the launch, or null
     uint64_t stats_groups;        // groups the stats buffer holds
     const uint32_t* fwd_list;     // appended to s.giant_list as they are (stage 0w's wide list)

@@ -439,7 +439,12 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
         // a lane steps in every iteration until it stops), so the hand-off
         // cap and the checks every 1024 iterations sit outside the inner loop
         uint64_t iter = 0;
-        const uint64_t cap = p.giant_cap ? p.giant_cap : ~0ull;
+        // (past tail_cap: the wave-mode tail launch searches it from the
+        // root -- its state DAG of ~17 levels costs less than hundreds of
+        // lane iterations; past giant_cap: the giant stage)
+        const uint64_t gcap = p.giant_cap ? p.giant_cap : ~0ull;
+        const uint64_t tcap = p.tail_cap && p.tail_list ? p.tail_cap : ~0ull;
+        const uint64_t cap = gcap < tcap ? gcap : tcap;
         uint32_t lane_iter = 0;   // (ST only)
         Written wr;
         wr.clear();
@@ -473,7 +478,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
             iter += k;
             if (__ballot(status < 0) == 0ull) break;
             if (iter >= cap) {
-                if (status < 0) status = QSMD_STATUS_HANDED_OFF;
+                if (status < 0) status = iter >= tcap && tcap < gcap ? QSMD_STATUS_TO_TAIL : QSMD_STATUS_HANDED_OFF;
                 break;
             }
             if (status < 0) {   // every 1024 iterations
@@ -500,6 +505,10 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
     }
     if (status == QSMD_STATUS_HANDED_OFF) {      // the giant stage searches it (exact, from the root)
         a.giant_list[atomicAdd(a.giant_count, 1u)] = h;
+        return;
+    }
+    if (status == QSMD_STATUS_TO_TAIL) {         // the tail launch searches it (exact, from the root)
+        p.tail_list[atomicAdd(p.tail_count, 1u)] = h;
         return;
     }
     note_failure(a, h, status);

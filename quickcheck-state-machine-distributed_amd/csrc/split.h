@@ -862,6 +862,7 @@ __device__ __forceinline__ void finish_call(const SplitArgs& p, int lane) {
     if (p.probe_host && lane == kProbeWide) p.probe_host[kProbeWide] = p.cnt[C_WIDE];
     if (p.probe_host && lane == kProbeBudget) p.probe_host[kProbeBudget] = p.probe_budget;
     if (p.probe_host && lane == kProbeN) p.probe_host[kProbeN] = (uint32_t)p.s.n_hist;
+    if (p.probe_host && lane == kProbeTail) p.probe_host[kProbeTail] = p.cnt[C_TAIL];
     if (p.probe_host && lane == kProbeWritten) p.probe_host[kProbeWritten] = 1u;
     // restore: buckets (and the early-exit ones), then the counters
     for (uint32_t i = (uint32_t)lane; i < kBuckets * kBucketWords; i += 64u) {

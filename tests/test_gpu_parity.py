@@ -140,7 +140,8 @@ def test_random_any_shape(ctx, model):
 
 DEFAULTS = {"stage0_budget": 32, "memo_after": 32, "stage0_grid": 65536, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
             "wave_grid": 0, "split_budget": 1024, "memo_lane_entries": 128, "memo_grid": 0, "split_xmemo": 1,
-            "memo_lds": 1, "memo_lds_entries": 64, "dag_states": 128, "memo_lds_cap": 0, "fold": 1, "resume_cap": 0}
+            "memo_lds": 1, "memo_lds_entries": 64, "dag_states": 128, "memo_lds_cap": 0, "fold": 1, "resume_cap": 0,
+            "tail_cap": 256, "tail_min": 65536}
 
 
 @pytest.fixture
@@ -293,6 +294,23 @@ def test_lane_mode(ctx, knobs, name, n, budget, max_nodes, entries, lds, lds_ent
           memo_lds_entries=lds_entries)
     hdr, ev, _ = gen.generate_config(name, 5, n)
     _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=max_nodes or 10**7)
+
+
+@pytest.mark.parametrize("cap", [1, 6, 40])
+@pytest.mark.parametrize("name,n,budget", [("bank_4x16_bugs", 20000, 8), ("bank_4x16", 20000, 4),
+                                           ("bank_6x24", 10000, 8), ("ticket_2x10", 20000, 4)])
+def test_lane_mode_tail(ctx, knobs, name, n, budget, cap):
+    """Lane mode's tail (api.hip tail_cap): the searches still running after
+    `cap` wavefront iterations go to a wave-mode launch after the heavy
+    stage and are searched there from the root (the state DAG, or the DFS
+    when it does not fit); with max_nodes inside them, BUDGET.  The first
+    call sets the heavy-count hint the tail needs (tail_min 0 here)."""
+    knobs(heavy_mode=1, memo_lds=0, tail_cap=cap, tail_min=0, stage0_budget=budget, stage0w_budget=budget)
+    hdr, ev, _ = gen.generate_config(name, 11, n)
+    mid = gen.CONFIGS[name]["model_id"]
+    for max_nodes in (10**7, 10**7, 60):
+        _compare(ctx, mid, hdr, ev, max_nodes=max_nodes)
+    assert ctx.get_param("tail_cap") == cap
 
 
 @pytest.mark.parametrize("name,n,budget,max_nodes", LANE_CASES)
