@@ -263,7 +263,13 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *                       a wave-mode launch after the heavy stage and is
  *                       searched there from the root (the state DAG), when
  *                       the last finished call sent at least tail_min
- *                       (default 65536) histories to the heavy stage
+ *                       (default 65536) histories, and a fifth of its batch,
+ *                       to the heavy stage (tail_min 0: whatever it sent)
+ *   "heavy_buckets"     1 (default): for the same long lists, the heavy
+ *                       stage forms its groups of 64 in order of predicted
+ *                       work (stage 0 records each heavy history's untried
+ *                       candidates on its stack; a counting sort orders the
+ *                       list); 0: in list order
  *   "resume_cap"        lane mode: stage 0's saved search states, slots per
  *                       heavy-list shard (0 = automatic: twice the last
  *                       call's heavy count per shard, at least 1024); a heavy

@@ -127,6 +127,9 @@ struct qsmd_ctx {
     // list whose longest searches set the stage's end); 0 = never
     uint64_t tail_cap = 256;
     uint64_t tail_min = 65536;
+    // the same long lists: the heavy stage forms its groups in order of
+    // predicted work (stage 0's heavy_key, memo.hip heavy_sort); 0 = never
+    uint64_t heavy_buckets = 1;
     // lane mode: stage 0's saved search states (80 B each), slots per heavy-
     // list shard: from the last call's heavy count (2x, at least 1024; an
     // eighth of the batch before the first call), or the knob resume_cap.  A
@@ -455,6 +458,9 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->tail_cap = value;
     } else if (n == "tail_min") {
         c->tail_min = value;
+    } else if (n == "heavy_buckets") {
+        if (value > 1) return fail(c, QSMD_ERR_ARG, "heavy_buckets: 0 or 1");
+        c->heavy_buckets = value;
     } else if (n == "memo_lds_cap") {       // diagnostic: force the LDS-refused path (the HBM tables)
         c->memo_lds_cap = value;
     } else if (n == "memo_lds") {
@@ -686,7 +692,15 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const bool fold = lane && c->fold && c->probe_valid && route == 0u && !sync_stages() &&
                       hint[0] == 0u && hint[2] == 0u;
     // lane mode's wave-mode tail launch (ctx.tail_cap): for a long heavy list
-    const bool tail = lane && c->tail_cap && c->probe_valid && heavy_hint >= c->tail_min && c->dag_states;
+    // (a list of at least tail_min and a fifth of the last batch: config 3's
+    // ~33 %, not config 2's 1.6 % at budget 20 or 9.6 % at the automatic 16,
+    // whose longest searches end before tail_cap -- the tail launch alone
+    // costs a lone call ~5 us, profiles/r06/inflight1.txt; tail_min 0: any list)
+    const bool long_list = c->probe_valid && (c->tail_min == 0 || (heavy_hint >= c->tail_min &&
+                                                                   5ull * heavy_hint >= hint[kProbeN]));
+    const bool tail = lane && c->tail_cap && long_list && c->dag_states;
+    // ... and its heavy list in order of predicted work
+    const bool buckets = lane && c->heavy_buckets && long_list && !(route & kSkip0);
 
     // ---- workspace: header, lists, giant records, tasks
     const bool want_w = (flags & QSMD_FLAG_WITNESS) && witness;
@@ -699,7 +713,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const size_t off_lw = off_h64 + lst;                 // stage 0w's deferred (wide) histories
     const size_t off_lg = off_lw + lst;                  // giants
     const size_t off_lt = off_lg + lst;                  // lane mode -> the wave-mode tail launch
-    const size_t off_gr = off_lt + lst;
+    const size_t off_ko = off_lt + lst;                  // heavy_sort: keys (u8 per heavy-list slot), order
+    const size_t off_gr = off_ko + (buckets ? align_up(kShards * cap32) + lst : 0);
     const size_t off_tk = off_gr + align_up(n_hist * sizeof(GiantRec));
     const size_t off_ts = off_tk + align_up(n_tk * sizeof(qsmd_task));
     const size_t off_tn = off_ts + align_up(n_tk);
@@ -739,6 +754,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     uint32_t* lw = reinterpret_cast<uint32_t*>(c->ws + off_lw);
     uint32_t* lg = reinterpret_cast<uint32_t*>(c->ws + off_lg);
     uint32_t* lt_list = reinterpret_cast<uint32_t*>(c->ws + off_lt);
+    uint8_t* hkey = buckets ? reinterpret_cast<uint8_t*>(c->ws + off_ko) : nullptr;
+    uint32_t* horder = buckets ? reinterpret_cast<uint32_t*>(c->ws + off_ko + align_up(kShards * cap32)) : nullptr;
     if (early && !nodes) nodes = reinterpret_cast<uint64_t*>(c->ws + off_nd);
 
     a.hdr = hdr;
@@ -819,6 +836,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.heavy_shard_cap = (uint32_t)cap32;
     a0.heavy_state = states;                 // (lane mode goes on from them)
     a0.heavy_state_cap = (uint32_t)rs_cap;
+    a0.heavy_key = hkey;
     // (below 2^31: a saved state keeps its node count in 32 bits)
     a0.stage0_budget = budget0 ? std::min<uint64_t>(budget0, 0x7FFFFFFFull) : ~0ull;
     a0.stamps = c->s0_stamps;
@@ -872,6 +890,7 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].lds_entries = lds_entries;
             mp[w].epoch = c->mt_epoch;
             mp[w].giant_cap = cap;
+            mp[w].order = w ? nullptr : horder;
             mp[w].tail_cap = tail ? c->tail_cap : 0u;
             mp[w].tail_list = tail ? lt_list : nullptr;
             mp[w].tail_count = cnt + C_TAIL;
@@ -879,6 +898,12 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].stats_groups = c->memo_stats ? c->memo_stats_groups : 0;
             mp[w].fwd_list = lw;                 // stage 0w's deferred histories: on to the giant stage
             mp[w].fwd_count = cnt + C_WIDE;
+        }
+        if (buckets) {   // (workgroups per shard for the last call's count; grid-stride beyond)
+            const uint64_t per = ((uint64_t)hint[1] / kShards + kSortChunkHost - 1) / kSortChunkHost;
+            HIP_TRY(c, launch_heavy_sort(shards, (uint32_t)cap32, hkey, cnt, horder,
+                                         (uint32_t)std::min<uint64_t>(std::max<uint64_t>(per, 1), 64), s),
+                    "heavy sort launch");
         }
         HIP_TRY(c, launch_memo(mp[0], mp[1], (uint32_t)mg, wide, lt, s, tm ? evs[3] : nullptr,
                                tm ? evs[4] : nullptr), "memo launch");
@@ -1224,6 +1249,8 @@ int qsmd_get_param(qsmd_ctx* c, const char* name, uint64_t* out) {
         *out = c->tail_cap;
     } else if (n == "tail_min") {
         *out = c->tail_min;
+    } else if (n == "heavy_buckets") {
+        *out = c->heavy_buckets;
     } else {
         return fail(c, QSMD_ERR_ARG, "unknown parameter");
     }

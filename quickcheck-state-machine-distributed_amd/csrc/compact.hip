@@ -150,6 +150,12 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
             if constexpr (G::EV == 32) {
                 if (heavy && a.heavy_state && at < a.heavy_state_cap)
                     dfs.save(a.heavy_state + ((uint64_t)k * a.heavy_state_cap + at) * kResumeWords, s_bal, lane);
+                // (long lists: the predicted work, by which the heavy stage's
+                // groups are formed -- internal.h heavy_key)
+                if (heavy && a.heavy_key) {
+                    const uint32_t u = dfs.untried_above();
+                    a.heavy_key[(uint64_t)k * a.heavy_shard_cap + at] = (uint8_t)(u < 255u ? u : 255u);
+                }
             }
         } else {
             wave_append(heavy, h, a.heavy_list, a.heavy_count, lane);

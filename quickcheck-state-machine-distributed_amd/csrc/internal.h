@@ -63,7 +63,9 @@ enum Cnt : uint32_t {
     C_WIDE,             // stage 0w -> wave mode's wide list (or, in lane mode, on to the giant stage)
     C_TAIL,             // lane mode -> the wave-mode tail launch (searches past tail_cap iterations)
     C_ZERO,             // always 0 (the tail launch's empty lists)
-    C_N = 32
+    C_KHIST = 32,       // heavy_sort: histories per predicted-work key (kKeys)
+    C_KCUR = 48,        // heavy_sort: each key's fill cursor
+    C_N = 64
 };
 
 // Stage 0's heavy list in kShards shards: a group of 64 appends to shard
@@ -77,6 +79,8 @@ enum Cnt : uint32_t {
 // 0's entries, then shard 1's, ...).
 // words of a saved stage-0 search state (LaneDFS::save / restore, lane.h)
 constexpr uint32_t kResumeWords = 20;
+constexpr uint32_t kKeys = 16;     // heavy_sort's key classes (a key past 15 counts as 15)
+constexpr uint32_t kSortChunkHost = 256;   // heavy_sort: entries per workgroup and pass (memo.hip kSortChunk)
 constexpr uint32_t kShards = 16;
 constexpr uint32_t kShardStride = 64;
 
@@ -138,6 +142,12 @@ struct SearchArgs {
                                   // positions past heavy_state_cap save nothing (the heavy stage starts
                                   // those at the root); null = no saved states
     uint32_t heavy_state_cap;
+    // stage 0, long heavy lists: a heavy history's predicted work (its
+    // untried candidates on the stack, LaneDFS::untried_above, saturated at
+    // 255) at its heavy-list position; memo.hip's heavy_sort orders the
+    // list by it, so histories of like remaining work share a wavefront
+    // (null: none)
+    uint8_t* heavy_key;
     uint64_t stage0_budget;
     uint32_t flags;
     uint32_t model_id;
@@ -323,6 +333,7 @@ struct MemoArgs {
     uint32_t lds_entries;         // LDS tables (lds_tables): entries per lane, a power of two <= 64
     uint32_t epoch;               // this call's tag (24 bits)
     uint64_t giant_cap;           // > 0: a search past this many iterations goes to s.giant_list
+    const uint32_t* order;        // G32 list: positions in heavy-key order (heavy_sort), or null: list order
     uint64_t tail_cap;            // > 0: a search past this many iterations goes to tail_list (wave mode)
     uint32_t* tail_list;
     uint32_t* tail_count;
@@ -337,6 +348,11 @@ struct MemoArgs {
 hipError_t launch_memo(const MemoArgs& p32, const MemoArgs& p64, uint32_t grid, bool wide, bool lds_tables,
                        hipStream_t s, hipEvent_t start, hipEvent_t stop);
 bool memo_lds_accepted(uint32_t model_id, uint32_t lds_entries, size_t cap);
+// stage 0's heavy list (shards: kShards counters, cap entries each) ordered
+// by heavy_key, highest first, into order (positions); cnt: the counters
+// (C_KHIST, C_KCUR zero on entry; finish_call restores them)
+hipError_t launch_heavy_sort(const uint32_t* shards, uint32_t cap, const uint8_t* key, uint32_t* cnt,
+                             uint32_t* order, uint32_t grid, hipStream_t s);
 
 hipError_t launch_gen(const qsmd_gen_params& p, uint64_t first, uint64_t n_hist, uint32_t ev_base, qsmd_hdr* hdr,
                       qsmd_event* events, uint8_t* bug_out, hipStream_t s);

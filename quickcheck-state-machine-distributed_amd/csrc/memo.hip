@@ -387,7 +387,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
     uint64_t r0 = 0, c0 = 0;
     uint32_t hits = 0;
     if constexpr (ST) r0 = __builtin_amdgcn_s_memrealtime();
-    const uint64_t pos = active ? list_pos(a.list_count, a.list_shard_cap, idx) : 0u;
+    const uint64_t pos = !active ? 0u : (p.order ? (uint64_t)p.order[idx] : list_pos(a.list_count, a.list_shard_cap, idx));
     const uint32_t h = active ? a.list[pos] : 0u;
     qsmd_hdr H;
     if (active) H = a.hdr[h];
@@ -571,6 +571,67 @@ __global__ __launch_bounds__(C_LANES, LT ? 1 : 3) void memo_search(MemoArgs p32,
         }
     }
     cnt.flush(p32.s.buckets, lane);
+}
+
+// ---------------------------------------------------------------- heavy_sort
+// Stage 0's heavy list ordered by predicted work (SearchArgs::heavy_key:
+// the untried candidates on the stack at the budget, correlation 0.84 with
+// a search's remaining lane iterations on config 3, tools/heavy_predictor.py),
+// highest key first, so the heavy stage's groups of 64 hold searches of like
+// length: lane utilisation 0.34 -> 0.49 on config 3.  Two launches, a
+// counting sort: per-key counts (each workgroup counts its share in LDS,
+// then one global atomic per key), then every workgroup reserves its range
+// of each key's run with one atomic per key and writes its positions there.
+// The order within a key follows the workgroups' reservations; the results
+// do not depend on it (each history's search is independent).  Workgroup x
+// of shard k takes that shard's entries x*256 .. x*256+255, grid-stride.
+constexpr uint32_t kSortChunk = kSortChunkHost;
+
+__device__ __forceinline__ uint32_t key_class(uint8_t key) { return key < kKeys - 1u ? key : kKeys - 1u; }
+
+__global__ __launch_bounds__(kSortChunk) void heavy_count(const uint32_t* shards, uint32_t cap, const uint8_t* key,
+                                                          uint32_t* cnt) {
+    __shared__ uint32_t hist[kKeys];
+    const uint32_t t = threadIdx.x, k = blockIdx.y;
+    if (t < kKeys) hist[t] = 0u;
+    __syncthreads();
+    const uint32_t n = shards[k * kShardStride];
+    for (uint32_t i = blockIdx.x * kSortChunk + t; i < n; i += gridDim.x * kSortChunk)
+        atomicAdd(&hist[key_class(key[(uint64_t)k * cap + i])], 1u);
+    __syncthreads();
+    if (t < kKeys && hist[t]) atomicAdd(cnt + C_KHIST + t, hist[t]);
+}
+
+__global__ __launch_bounds__(kSortChunk) void heavy_scatter(const uint32_t* shards, uint32_t cap, const uint8_t* key,
+                                                            uint32_t* cnt, uint32_t* order) {
+    __shared__ uint32_t start[kKeys], hist[kKeys];
+    const uint32_t t = threadIdx.x, k = blockIdx.y;
+    const uint32_t n = shards[k * kShardStride];
+    // each key's run: the keys above it first
+    if (t < kKeys) {
+        uint32_t p = 0u;
+        for (uint32_t b = kKeys - 1u; b > t; --b) p += cnt[C_KHIST + b];
+        start[t] = p;
+    }
+    for (uint32_t base = blockIdx.x * kSortChunk; base < n; base += gridDim.x * kSortChunk) {
+        if (t < kKeys) hist[t] = 0u;
+        __syncthreads();
+        const uint32_t i = base + t;
+        const uint32_t b = i < n ? key_class(key[(uint64_t)k * cap + i]) : 0u;
+        const uint32_t rank = i < n ? atomicAdd(&hist[b], 1u) : 0u;
+        __syncthreads();
+        if (t < kKeys && hist[t]) hist[t] = start[t] + atomicAdd(cnt + C_KCUR + t, hist[t]);
+        __syncthreads();
+        if (i < n) order[hist[b] + rank] = k * cap + i;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_heavy_sort(const uint32_t* shards, uint32_t cap, const uint8_t* key, uint32_t* cnt,
+                             uint32_t* order, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(heavy_count, dim3(grid, kShards), dim3(kSortChunk), 0, s, shards, cap, key, cnt);
+    hipLaunchKernelGGL(heavy_scatter, dim3(grid, kShards), dim3(kSortChunk), 0, s, shards, cap, key, cnt, order);
+    return hipGetLastError();
 }
 
 template <uint32_t MODEL>

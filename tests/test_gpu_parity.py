@@ -141,7 +141,7 @@ def test_random_any_shape(ctx, model):
 DEFAULTS = {"stage0_budget": 32, "memo_after": 32, "stage0_grid": 65536, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
             "wave_grid": 0, "split_budget": 1024, "memo_lane_entries": 128, "memo_grid": 0, "split_xmemo": 1,
             "memo_lds": 1, "memo_lds_entries": 64, "dag_states": 128, "memo_lds_cap": 0, "fold": 1, "resume_cap": 0,
-            "tail_cap": 256, "tail_min": 65536}
+            "tail_cap": 256, "tail_min": 65536, "heavy_buckets": 1}
 
 
 @pytest.fixture
@@ -311,6 +311,24 @@ def test_lane_mode_tail(ctx, knobs, name, n, budget, cap):
     for max_nodes in (10**7, 10**7, 60):
         _compare(ctx, mid, hdr, ev, max_nodes=max_nodes)
     assert ctx.get_param("tail_cap") == cap
+
+
+@pytest.mark.parametrize("buckets,resume_cap", [(1, 0), (1, 3), (0, 0)])
+@pytest.mark.parametrize("name,n,budget", [("bank_4x16_bugs", 30000, 12), ("bank_4x16", 30000, 4),
+                                           ("ticket_2x10", 20000, 3)])
+def test_heavy_buckets(ctx, knobs, name, n, budget, buckets, resume_cap):
+    """The heavy stage's groups formed in order of predicted work (stage 0
+    writes each heavy history's untried candidates on the stack, memo.hip's
+    heavy_sort orders the list by them) against list order, with the saved
+    states' slots cut to 3 per shard (the rest start at the root), lane
+    mode, no tail; three calls, the first setting the heavy-count hint the
+    ordering needs (tail_min 0)."""
+    knobs(heavy_mode=1, memo_lds=0, tail_cap=0, tail_min=0, heavy_buckets=buckets, resume_cap=resume_cap,
+          stage0_budget=budget, stage0w_budget=budget)
+    hdr, ev, _ = gen.generate_config(name, 13, n)
+    mid = gen.CONFIGS[name]["model_id"]
+    for max_nodes in (10**7, 10**7, 80):
+        _compare(ctx, mid, hdr, ev, max_nodes=max_nodes)
 
 
 @pytest.mark.parametrize("name,n,budget,max_nodes", LANE_CASES)
