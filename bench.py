@@ -521,7 +521,7 @@ def main():
                     help="calls in flight (one context + stream each); 0 = 4 (the extra configs: 3)")
     ap.add_argument("--device-gen", action="store_true",
                     help="generate the batch on the GPU (qsmd_gen_batch_device; same histories as the host generator)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r05", "stage0_pmc.json"),
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "r06", "stage0_pmc.json"),
                     help="PMC summary of the search kernels (profiles/summarize_pmc.py) for the roofline fields")
     ap.add_argument("--early-exit", action="store_true",
                     help="time BASELINE config 3's early-termination path instead (bank_4x16_bugs by default, "
