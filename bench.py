@@ -508,7 +508,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the extra BASELINE configs")
     ap.add_argument("--stage0-budget", type=int, default=None,
-                    help="stage-0 node budget (default 18 with calls in flight, the library's otherwise)")
+                    help="stage-0 node budget (default 20 with calls in flight, the library's otherwise)")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=VALUE",
                     help="qsmd_set_param on every context (tuning; repeatable)")
     ap.add_argument("--memo", action="store_true", help="QSMD_FLAG_MEMO (node counts become 'explored')")

@@ -216,8 +216,8 @@ int qsmd_set_stage0_grid(qsmd_ctx* ctx, uint64_t max_blocks);
  * history with an exact-count state memo, from the saved search state; or
  * one wavefront per history), so one long search does not hold 63 idle
  * lanes.  Default (until set; knob "stage0_budget_auto" 1 restores it):
- * automatic -- 32, or 16 while the context's last finished call sent fewer
- * than 1 in 50 histories to the heavy stage, back to 32 above 1 in 5.
+ * automatic -- 24, or 16 while the context's last finished call sent fewer
+ * than 1 in 50 histories to the heavy stage, back to 24 above 1 in 5.
  * Results are unchanged. */
 int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
 

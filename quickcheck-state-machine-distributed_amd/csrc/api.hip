@@ -75,12 +75,13 @@ struct qsmd_ctx {
     uint64_t time_limit_ms = 120000;   // safety net per search launch
     uint64_t stage0_max_grid = 65536;  // tuning: cap on stage-0 workgroups (grid-stride beyond)
     uint64_t stage0_budget = 32;       // stage-0 node budget before the heavy stage (when not automatic)
-    // automatic stage-0 budget (until a budget is set): 32, or 16 while the
+    // automatic stage-0 budget (until a budget is set): 24, or 16 while the
     // last finished call's stage 0 sent few histories to the heavy stage --
     // one call at a time on config 2: 4.78 vs 4.59e9 (the heavy list long
     // enough for lane mode, whose tail is no longer than wave mode's, behind
-    // a shorter stage 0); config 3's bug-laden batches keep 32 (their heavy
-    // fraction at 16 is far above the threshold)
+    // a shorter stage 0); config 3's bug-laden batches keep 24 (their heavy
+    // fraction at 16 is far above the threshold; 24 vs 32 with the ordered
+    // groups and the tail launch: 1.55 vs 1.49e9, profiles/r06/xbudget)
     bool s0_auto = true;
     uint64_t stage0w_budget = 32;      // stage-0w node budget before the heavy stage
     uint64_t split_budget = 1024;      // giant stage: whole-search iterations = 16x, heavy-stage cap = 64x
@@ -378,11 +379,11 @@ void qsmd_close(qsmd_ctx* c) {
     delete c;
 }
 
-static constexpr uint64_t kAutoLo = 16, kAutoHi = 32;
+static constexpr uint64_t kAutoLo = 16, kAutoHi = 24;
 
 // the stage-0 budget of this call: the set one, or (automatic) from the last
-// finished call's probe -- at 16, back to 32 once more than 1 in 5 of its
-// histories went on to the heavy stage; at 32, down to 16 while fewer than 1
+// finished call's probe -- at 16, back to 24 once more than 1 in 5 of its
+// histories went on to the heavy stage; at 24, down to 16 while fewer than 1
 // in 50 did (the gap between the two keeps a batch from alternating)
 static uint64_t stage0_budget_of(const qsmd_ctx* c, const uint32_t* hint) {
     if (!c->s0_auto) return c->stage0_budget;

@@ -79,17 +79,23 @@ def test_timing_events():
 
 
 def test_automatic_stage0_budget():
-    """The automatic stage-0 budget (the default until a budget is set): 32,
-    16 after a call whose heavy list was short, back to 32 after one whose
+    """The automatic stage-0 budget (the default until a budget is set): 24,
+    16 after a call whose heavy list was short, back to 24 after one whose
     list was long.  Alternating config-2 batches (few heavy histories) and
     bug-laden config-3 batches (many) moves it both ways; each call's first
     heavy stage is then sized for the other budget's list (wave mode with a
-    long list, lane mode with a short one).  Results stay the oracle's."""
+    long list, lane mode with a short one).  Results stay the oracle's, and
+    `stage0_budget_last` follows the hysteresis: config 2 at 24 sends < 1 in
+    50 to the heavy stage (-> 16), config 3 at 16 > 1 in 5 (-> 24), config 2
+    at 16 ~1 in 10 (stays)."""
     c = device.Context(0)
     try:
         batches = [(name, gen.generate_config(name, 9, 30000)) for name in ("bank_4x16", "bank_4x16_bugs")]
+        used = []
         for name, (hdr, ev, _) in batches * 3 + batches[:1] * 2:
             _compare(c, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+            used.append(c.get_param("stage0_budget_last"))
+        assert used == [24, 16, 24, 16, 24, 16, 24, 16], used
     finally:
         c.close()
 
