@@ -499,6 +499,11 @@ struct LaneDFS {
                             // 32: none -- a BUDGET from the time limit, compact.hip run_search)
     uint64_t nodes;
     StackN<G::LEVELS / 4> stk;
+    // (Bank, the memo stage's slot hash: memo.hip) the XOR over accounts q of
+    // balance q rotated right by 4q, kept by undo / try_next when FOLD -- the
+    // probe's slot from registers, the balances read only for a probe that
+    // can hit.  Unused (and not computed) by the compact stages.
+    uint32_t fold;
 
     // events whose pid equals the pid of event j (bit-sliced compare); the
     // bits beyond the history are not cleared -- every use ANDs the result
@@ -541,7 +546,7 @@ struct LaneDFS {
     // a history shared by the wavefront: STRIDE = 1)
     // Undo the last level: restore the parent node's state exactly
     // (remaining events, model); returns the candidate the level went through.
-    template <int STRIDE>
+    template <int STRIDE, bool FOLD = false>
     __device__ __forceinline__ uint32_t undo(const uint32_t* evc, int32_t (*s_bal)[C_LANES], int lane) {
         --depth;
         const uint32_t st = stk.top();
@@ -569,6 +574,10 @@ struct LaneDFS {
             const int32_t fb = tr ? rb : bb;
             s_bal[ib][lane] = fb;                  // a no-op unless Transfer
             s_bal[ia][lane] = ra;                  // written last (ia == ib)
+            if constexpr (FOLD) {
+                const uint32_t da = (uint32_t)(ba ^ ra), db = same ? 0u : (uint32_t)(bb ^ fb);
+                fold ^= __builtin_amdgcn_alignbit(da, da, ia << 2) ^ __builtin_amdgcn_alignbit(db, db, ib << 2);
+            }
             // the existence bits of a (and b for Transfer) back to the stack's
             const uint32_t A = 1u << ia, B = tr ? 1u << ib : 0u;
             ex = (ex & ~A) | (A & (uint32_t)pam);
@@ -611,7 +620,7 @@ struct LaneDFS {
     }
 
     // ---- try the next candidate: straight-line, predicated
-    template <int STRIDE>
+    template <int STRIDE, bool FOLD = false>
     __device__ __forceinline__ int try_next(const SearchArgs& a, const uint32_t* evc,
                                             int32_t (*s_bal)[C_LANES], int lane, uint64_t limit) {
         const uint32_t j = m_ctz(cand);
@@ -662,7 +671,13 @@ struct LaneDFS {
             const int32_t fb = tr ? (same ? na : (bal_b & exbm)) + m : bo;
             s_bal[ia][lane] = ok ? na : bal_a;
             s_bal[ib][lane] = ok ? fb : bal_b;
-            const int32_t va = same ? fb : na;
+            const int32_t va = same ? fb : na;     // a's value after the step
+            if constexpr (FOLD) {
+                const uint32_t da = (uint32_t)(bal_a ^ va), db = same ? 0u : (uint32_t)(bal_b ^ fb);
+                const uint32_t df =
+                    __builtin_amdgcn_alignbit(da, da, ia << 2) ^ __builtin_amdgcn_alignbit(db, db, ib << 2);
+                fold ^= ok ? df : 0u;
+            }
             ex = lshl_or((ok & !chk) ? 1u : 0u, ia, ex);
             ex = lshl_or((ok & tr) ? 1u : 0u, ib, ex);
             // ok => the invariant held before the step and absent accounts

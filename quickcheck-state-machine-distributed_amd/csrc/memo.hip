@@ -101,10 +101,47 @@ __device__ __forceinline__ KeyRaw<MODEL> memo_key_raw(int32_t (*s_bal)[C_LANES],
     return r;
 }
 
+// Bank: LaneDFS::fold of the raw balances (the XOR over accounts q of
+// balance q rotated right by 4q; undo / try_next keep it from here on)
+template <uint32_t MODEL>
+__device__ __forceinline__ uint32_t fold_of(const KeyRaw<MODEL>& r) {
+    uint32_t f = 0u;
+    if constexpr (MODEL == QSMD_MODEL_BANK) {
+#pragma unroll
+        for (int q = 0; q < QSMD_BANK_MAX_ACCOUNTS; ++q) f ^= __builtin_amdgcn_alignbit(r.b[q], r.b[q], 4u * q);
+    }
+    return f;
+}
+
+// The Ticket model's key word: the model after the levels 0 .. depth-1 (the
+// formula of LaneDFS::try_next), just | n << 1
+template <uint32_t MODEL>
+__device__ __forceinline__ uint32_t ticket_word(uint32_t RS, uint32_t depth, const SearchArgs& a) {
+    const uint32_t just = RS ? 1u : a.m0_just;
+    const int32_t n = RS ? (int32_t)(depth - 1u - (31u - __builtin_clz(RS | 1u)))
+                         : (int32_t)a.m0_val[0] + (a.m0_just ? (int32_t)depth : 0);
+    return just | (just ? ((uint32_t)n & 0xFFFFu) << 1 : 0u);
+}
+
+// The slot of a state from registers: the model's word (Bank: the balances'
+// fold and the existing accounts; Ticket: the key word) rotated into the
+// remaining set, then one multiplicative hash (one quarter-rate multiply)
 template <uint32_t MODEL, class G>
-__device__ __forceinline__ LaneKey<MODEL, G> memo_key_of(const KeyRaw<MODEL>& r, typename G::M rem, uint32_t ex,
-                                                         uint32_t RS, uint32_t depth, const SearchArgs& a,
-                                                         uint32_t epoch, SlotHash sh) {
+__device__ __forceinline__ uint32_t memo_slot(uint32_t fold, typename G::M rem, uint32_t ex, uint32_t RS,
+                                              uint32_t depth, const SearchArgs& a, SlotHash sh) {
+    const uint32_t v = MODEL == QSMD_MODEL_BANK ? fold ^ ex : ticket_word<MODEL>(RS, depth, a);
+    uint32_t t = (uint32_t)rem ^ __builtin_amdgcn_alignbit(v, v, 13);
+    if constexpr (G::EV == 64) {
+        const uint32_t hi = (uint32_t)((uint64_t)rem >> 32);
+        t ^= __builtin_amdgcn_alignbit(hi, hi, 7);
+    }
+    return (t * 0x9E3779B1u) >> sh.sh;
+}
+
+template <uint32_t MODEL, class G>
+__device__ __forceinline__ LaneKey<MODEL, G> memo_key_of(const KeyRaw<MODEL>& r, uint32_t fold, typename G::M rem,
+                                                         uint32_t ex, uint32_t RS, uint32_t depth,
+                                                         const SearchArgs& a, uint32_t epoch, SlotHash sh) {
     LaneKey<MODEL, G> k;
     k.rem_lo = (uint32_t)rem;
     k.rem_hi = G::EV == 64 ? (uint32_t)((uint64_t)rem >> 32) : 0u;
@@ -113,22 +150,12 @@ __device__ __forceinline__ LaneKey<MODEL, G> memo_key_of(const KeyRaw<MODEL>& r,
 #pragma unroll
         for (int q = 0; q < 4; ++q) k.m[q] = __builtin_amdgcn_perm(r.b[2 * q + 1], r.b[2 * q], 0x05040100u);
     } else {
-        // model after the levels 0 .. depth-1 (the formula of LaneDFS::try_next)
         ex = 0u;
-        const uint32_t just = RS ? 1u : a.m0_just;
-        const int32_t n = RS ? (int32_t)(depth - 1u - (31u - __builtin_clz(RS | 1u)))
-                             : (int32_t)a.m0_val[0] + (a.m0_just ? (int32_t)depth : 0);
-        k.m[0] = just | (just ? ((uint32_t)n & 0xFFFFu) << 1 : 0u);
+        k.m[0] = ticket_word<MODEL>(RS, depth, a);
         k.m[1] = k.m[2] = k.m[3] = 0u;
     }
     k.w1 = (epoch & 0xFFFFFFu) | (ex << 24);
-    // the model words rotated apart and folded into the remaining set, then
-    // one multiplicative hash (one quarter-rate multiply per key)
-    const uint32_t v = (k.m[0] ^ ex ^ __builtin_amdgcn_alignbit(k.m[1], k.m[1], 8)) ^
-                       (__builtin_amdgcn_alignbit(k.m[2], k.m[2], 16) ^ __builtin_amdgcn_alignbit(k.m[3], k.m[3], 24));
-    uint32_t t = k.rem_lo ^ __builtin_amdgcn_alignbit(v, v, 13);
-    if constexpr (G::EV == 64) t ^= __builtin_amdgcn_alignbit(k.rem_hi, k.rem_hi, 7);
-    k.slot = (t * 0x9E3779B1u) >> sh.sh;
+    k.slot = memo_slot<MODEL, G>(fold, rem, ex, RS, depth, a, sh);
     return k;
 }
 
@@ -136,7 +163,8 @@ template <uint32_t MODEL, class G>
 __device__ __forceinline__ LaneKey<MODEL, G> memo_key(const LaneDFS<MODEL, G>& d, const SearchArgs& a,
                                                       int32_t (*s_bal)[C_LANES], int lane, uint32_t epoch,
                                                       SlotHash sh) {
-    return memo_key_of<MODEL, G>(memo_key_raw<MODEL, G>(s_bal, lane), d.rem, d.ex, d.RS, d.depth, a, epoch, sh);
+    return memo_key_of<MODEL, G>(memo_key_raw<MODEL, G>(s_bal, lane), d.fold, d.rem, d.ex, d.RS, d.depth, a, epoch,
+                                 sh);
 }
 
 template <uint32_t MODEL, class G>
@@ -218,11 +246,12 @@ struct Written {
 //   [0..2] realtime at start / staged / end  [3] max DFS iterations over the
 //   lanes  [4] their sum  [5] memo hits  [6] histories  [7] shader cycles of
 //   the search loop (max over the lanes)
-//   [8..12] shader cycles the wavefront spent in the iteration's phases, each
+//   [8..11] shader cycles the wavefront spent in the iteration's phases, each
 //   drained of its memory operations before its end stamp (so latency lands
 //   in the phase that issued it): [8] backtrack (entry count, memo count,
-//   undo) [9] try_next [10] memo key [11] HBM probe [12] hit / pending
-//   entry / level record
+//   undo) [9] try_next [10] memo slot [11] HBM probe (the key's balances and
+//   the entry)  [12] wave iterations in which some lane's LaneDFS::fold
+//   differs from its balances' (a consistency check: 0)
 //   [13] wave iterations with a backtrack [14] with an HBM probe [15] wave
 //   iterations
 constexpr uint32_t kMemoStatsWords = 16;
@@ -245,7 +274,7 @@ struct PhaseClock {
         if (lane == (int)__builtin_ctzll(__ballot(1))) acc[k] += t - t0;
     }
     __device__ __forceinline__ void count(int k, bool any, int lane) {
-        if (lane == 0 && any) acc[k] += 1;
+        if (lane == (int)__builtin_ctzll(__ballot(1)) && any) acc[k] += 1;
     }
 };
 
@@ -284,8 +313,8 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
         uint32_t ent = entry[(d.depth - 1u) * C_LANES];
         KeyRaw<MODEL> raw = memo_key_raw<MODEL, G>(s_bal, lane);
         const M rem0 = d.rem;
-        const uint32_t ex0 = d.ex, RS0 = d.RS, dep0 = d.depth;
-        const uint32_t j = d.template undo<C_LANES>(evc, s_bal, lane);
+        const uint32_t ex0 = d.ex, RS0 = d.RS, dep0 = d.depth, fold0 = d.fold;
+        const uint32_t j = d.template undo<C_LANES, true>(evc, s_bal, lane);
         // (the key's reads complete here, not sunk into the branch below: the
         // compiler issues them beside the undo's)
         if constexpr (MODEL == QSMD_MODEL_BANK)
@@ -297,7 +326,7 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
         d.cand = cands(d.rem, d.INV, d.RESP) & mask_above(j, (M)0);
         d.found = 1u;
         if (rec) {
-            const LaneKey<MODEL, G> k = memo_key_of<MODEL, G>(raw, rem0, ex0, RS0, dep0, a, epoch, sh);
+            const LaneKey<MODEL, G> k = memo_key_of<MODEL, G>(raw, fold0, rem0, ex0, RS0, dep0, a, epoch, sh);
             if constexpr (LT) {
                 memo_insert_lds<MODEL, G>(tab, k, h, cnt);
             } else {
@@ -310,23 +339,34 @@ __device__ __forceinline__ int memo_step(LaneDFS<MODEL, G>& d, const SearchArgs&
     if (d.cand) {
         const uint32_t dep0 = d.depth;
         if constexpr (ST) t0 = ph->start();
-        status = d.template try_next<C_LANES>(a, evc, s_bal, lane, limit);
-        if constexpr (ST) ph->stop(1, t0, lane);
-        if (d.depth > dep0 && status < 0) {       // entered a new node (and the search goes on)
-            entry[dep0 * C_LANES] = (uint32_t)d.nodes;
+        status = d.template try_next<C_LANES, true>(a, evc, s_bal, lane, limit);
+        if constexpr (ST) {
+            ph->stop(1, t0, lane);
+            if constexpr (MODEL == QSMD_MODEL_BANK)
+                ph->count(4, __ballot(fold_of<MODEL>(memo_key_raw<MODEL, G>(s_bal, lane)) != d.fold) != 0ull, lane);
         }
+        // the count at entry of the node a descent enters: stored whether or
+        // not this try descended (the slot belongs to the current node's
+        // next child, read only on leaving a child entered after this store)
+        entry[dep0 * C_LANES] = (uint32_t)d.nodes;
         if (memo && d.depth > dep0 && status < 0) {
-            if constexpr (ST) t0 = ph->start();
-            const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, sh);
-            if constexpr (ST) ph->stop(2, t0, lane);
             uint32_t cnt = 0;
             bool hit = false;
             if constexpr (LT) {
+                if constexpr (ST) t0 = ph->start();
+                const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, sh);
+                if constexpr (ST) ph->stop(2, t0, lane);
                 hit = memo_lookup_lds<MODEL, G>(tab, k, h, cnt);
             } else {
-                if constexpr (ST) ph->count(6, __ballot(wr.maybe(k.slot)) != 0ull, lane);
-                if (wr.maybe(k.slot)) {
+                // the slot from registers; the key's balances only for a
+                // probe of a slot this lane wrote for this history
+                if constexpr (ST) t0 = ph->start();
+                const uint32_t slot = memo_slot<MODEL, G>(d.fold, d.rem, d.ex, d.RS, d.depth, a, sh);
+                if constexpr (ST) ph->stop(2, t0, lane);
+                if constexpr (ST) ph->count(6, __ballot(wr.maybe(slot)) != 0ull, lane);
+                if (wr.maybe(slot)) {
                     if constexpr (ST) t0 = ph->start();
+                    const LaneKey<MODEL, G> k = memo_key<MODEL, G>(d, a, s_bal, lane, epoch, sh);
                     hit = memo_lookup<MODEL, G>(tab, k, h, cnt);
                     if constexpr (ST) ph->stop(3, t0, lane);
                 }
@@ -432,6 +472,7 @@ __device__ __forceinline__ void memo_group(const MemoArgs& p, uint64_t base, Mem
                 for (uint32_t d = 0; d < dfs.depth; ++d) L.entry[d][lane] = kNoEntry;
             }
         }
+        dfs.fold = fold_of<MODEL>(memo_key_raw<MODEL, G>(L.bal, lane));
     }
     if (search) {
         bool skip = false;

@@ -87,9 +87,11 @@ def main():
                           "histories": int(q[worst, 6])},
     }
     wave_it = max(int(q[:, 15].sum()), 1)
-    names = ("backtrack", "try_next", "memo_key", "hbm_probe", "hit_insert_level")
+    names = ("backtrack", "try_next", "memo_slot", "hbm_probe")
     out["phase_cycles_per_wave_iteration"] = {k: round(float(q[:, 8 + i].sum()) / wave_it, 0)
                                               for i, k in enumerate(names)}
+    # LaneDFS::fold against the balances it folds, after every try (must be 0)
+    out["fold_mismatch_wave_iterations"] = int(q[:, 12].sum())
     out["wave_iterations"] = wave_it
     out["fraction_of_wave_iterations"] = {"with_backtrack": round(float(q[:, 13].sum()) / wave_it, 3),
                                           "with_hbm_probe": round(float(q[:, 14].sum()) / wave_it, 3)}
