@@ -277,7 +277,10 @@ void stage_done(const char* name, hipStream_t s, const uint32_t* cnt) {
         uint32_t sh[kShards * kShardStride];
         (void)hipMemcpy(sh, reinterpret_cast<const char*>(cnt) - kOffCnt + kOffShards, sizeof sh,
                         hipMemcpyDeviceToHost);
-        for (uint32_t k = 0; k < kShards; ++k) h[C_HEAVY32] += sh[k * kShardStride];
+        for (uint32_t k = 0; k < kShards; ++k) {
+            h[C_HEAVY32] += sh[k * kShardStride];
+            h[C_DEFER] += sh[k * kShardStride + kDeferShardWord];
+        }
     }
     const auto t = std::chrono::steady_clock::now();
     std::fprintf(stderr, "[qsmd] %-8s %s %.3f ms  defer %u heavy %u/%u giants %u timed %u tasks %u/%u\n", name,
@@ -708,8 +711,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     const uint64_t n_tk = (uint64_t)SPLIT_VARIANTS * kTaskCap;
     const size_t lst = align_up(n_hist * 4 + 4);
     const size_t off_l0 = kWsHeader;                     // stage 0 -> stage 0w
-    const uint64_t cap32 = shard_cap(n_hist);            // stage 0's heavy list: kShards shards (internal.h)
-    const size_t off_h32 = off_l0 + lst;                 // heavy lists
+    const uint64_t cap32 = shard_cap(n_hist);            // stage 0's heavy and deferred lists: kShards shards (internal.h)
+    const size_t off_h32 = off_l0 + align_up(kShards * cap32 * 4 + 4);   // heavy lists
     const size_t off_h64 = off_h32 + align_up(kShards * cap32 * 4 + 4);
     const size_t off_lw = off_h64 + lst;                 // stage 0w's deferred (wide) histories
     const size_t off_lg = off_lw + lst;                  // giants
@@ -831,7 +834,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     a0.list = nullptr;
     a0.list_count = nullptr;
     a0.defer_list = l0;
-    a0.defer_count = cnt + C_DEFER;
+    a0.defer_count = shards + kDeferShardWord;
+    a0.defer_shard_cap = (uint32_t)cap32;
     a0.heavy_list = h32;
     a0.heavy_count = shards;
     a0.heavy_shard_cap = (uint32_t)cap32;
@@ -855,7 +859,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     // ---- stage 0w: the rest, <= 64 events (beyond: the giant stage)
     SearchArgs aw = a;
     aw.list = (route & kSkip0) ? nullptr : l0;               // (null: every history of the batch)
-    aw.list_count = (route & kSkip0) ? nullptr : cnt + C_DEFER;
+    aw.list_count = (route & kSkip0) ? nullptr : shards + kDeferShardWord;
+    aw.list_shard_cap = (route & kSkip0) ? 0u : (uint32_t)cap32;
     aw.defer_list = lw;                      // (wave mode searches most of them; the rest: giants)
     aw.defer_count = cnt + C_WIDE;
     aw.heavy_list = h64;
@@ -881,8 +886,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
             mp[w].s = a;
             // (folded: no stage 0w ran, G64 groups are stage 0's deferred histories)
             mp[w].s.list = w ? (fold ? l0 : h64) : h32;
-            mp[w].s.list_count = w ? cnt + (fold ? C_DEFER : C_HEAVY64) : shards;
-            mp[w].s.list_shard_cap = w ? 0u : (uint32_t)cap32;
+            mp[w].s.list_count = w ? (fold ? shards + kDeferShardWord : cnt + C_HEAVY64) : shards;
+            mp[w].s.list_shard_cap = w && !fold ? 0u : (uint32_t)cap32;
             mp[w].table = reinterpret_cast<uint32_t*>(c->mt + (w ? slots * 32 : 0));
             mp[w].entries = (uint32_t)c->mt_entries;
             mp[w].memo_after = (uint32_t)std::min<uint64_t>(c->memo_after, 0xFFFFFFFFull);

@@ -75,7 +75,7 @@ __device__ __forceinline__ int run_search(DFS& dfs, const SearchArgs& a, const u
 template <uint32_t MODEL, class G>
 __device__ __forceinline__ int stage_fresh(const SearchArgs& a, bool fresh, uint32_t h, uint32_t (*s_ev)[C_LANES],
                                            int32_t (*s_bal)[C_LANES], int lane, LaneDFS<MODEL, G>& dfs,
-                                           qsmd_hdr& H) {
+                                           qsmd_hdr& H, uint32_t shard) {
     using M = typename G::M;
     if (fresh) H = a.hdr[h];
     else H = qsmd_hdr{0, 0, 0, 0, 0, 0};
@@ -98,7 +98,13 @@ __device__ __forceinline__ int stage_fresh(const SearchArgs& a, bool fresh, uint
     s.ok = s.ok && enc_ok;
 
     const bool defer = enc_ok && (!small || (s.ok && !s.fits));
-    wave_append(defer, h, a.defer_list, a.defer_count, lane);   // -> the next stage
+    // -> the next stage (stage 0: the group's shard, as the heavy list's --
+    // one counter for the batch serialised a wide batch's appends)
+    if (a.defer_shard_cap)
+        wave_append(defer, h, a.defer_list + (uint64_t)shard * a.defer_shard_cap,
+                    a.defer_count + shard * kShardStride, lane);
+    else
+        wave_append(defer, h, a.defer_list, a.defer_count, lane);
     if (!fresh || defer) return -2;          // (dfs untouched: the lane may be searching)
     dfs.depth = 0;
     dfs.nodes = 0;
@@ -119,7 +125,7 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
     __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
 
     const int lane = threadIdx.x;
-    const uint64_t total = a.list ? (uint64_t)*a.list_count : a.n_hist;
+    const uint64_t total = a.list ? (uint64_t)list_total(a.list_count, a.list_shard_cap) : a.n_hist;
     if ((uint64_t)blockIdx.x * C_LANES >= total) return;   // (stage 0w of a call that deferred nothing)
     WaveCounters cnt;
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -131,10 +137,11 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
     for (uint64_t base = (uint64_t)blockIdx.x * C_LANES; base < total; base += (uint64_t)gridDim.x * C_LANES) {
         const uint64_t idx = base + lane;
         const bool active = idx < total;
-        const uint32_t h = active ? (a.list ? a.list[idx] : (uint32_t)idx) : 0u;
+        const uint32_t h = active ? (a.list ? list_at(a.list, a.list_count, a.list_shard_cap, idx) : (uint32_t)idx) : 0u;
+        const uint32_t shard = (uint32_t)((base / C_LANES) % kShards);
         qsmd_hdr H;
         LaneDFS<MODEL, G> dfs;
-        int status = stage_fresh<MODEL, G>(a, active, h, s_ev, s_bal, lane, dfs, H);
+        int status = stage_fresh<MODEL, G>(a, active, h, s_ev, s_bal, lane, dfs, H, shard);
         const bool live = status != -2;     // (-2: no history here, or handed to the next stage)
         const bool search = status == -1;
         const uint32_t n_ev = H.n_ev;
@@ -144,7 +151,7 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
         // over the stage budget (not the caller's): searched again by the heavy stage
         const bool heavy = tiered && status == QSMD_STATUS_BUDGET && dfs.nodes >= limit;
         if (a.heavy_shard_cap) {    // (stage 0: the group's shard, internal.h)
-            const uint32_t k = (uint32_t)((base / C_LANES) % kShards);
+            const uint32_t k = shard;
             const uint32_t at = wave_append(heavy, h, a.heavy_list + (uint64_t)k * a.heavy_shard_cap,
                                             a.heavy_count + k * kShardStride, lane);
             if constexpr (G::EV == 32) {

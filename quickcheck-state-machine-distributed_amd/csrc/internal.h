@@ -70,7 +70,8 @@ enum Cnt : uint32_t {
 
 // Stage 0's heavy list in kShards shards: a group of 64 appends to shard
 // (group % kShards), whose counter sits kShardStride words (256 B) from the
-// next one.  One counter for the whole batch serialised the appends (one
+// next one (its deferred list the same way, the counter one word after the
+// heavy list's: kDeferShardWord).  One counter for the whole batch serialised the appends (one
 // returning atomic per wavefront on one address): lone stage 0 at node
 // budget 20 took 0.171 ms with it and 0.105 ms without any append.  Shard k
 // holds at most ceil(groups / kShards) groups' histories, so shard k's
@@ -83,6 +84,7 @@ constexpr uint32_t kKeys = 16;     // heavy_sort's key classes (a key past 15 co
 constexpr uint32_t kSortChunkHost = 256;   // heavy_sort: entries per workgroup and pass (memo.hip kSortChunk)
 constexpr uint32_t kShards = 16;
 constexpr uint32_t kShardStride = 64;
+constexpr uint32_t kDeferShardWord = 1;   // stage 0's deferred list: shard k's counter at [k * kShardStride + 1]
 
 __host__ __device__ inline uint64_t shard_cap(uint64_t n_hist) {
     return ((n_hist + 63) / 64 + kShards - 1) / kShards * 64;
@@ -132,6 +134,7 @@ struct SearchArgs {
     // histories this stage cannot hold go to defer_list
     uint32_t* defer_list;
     uint32_t* defer_count;
+    uint32_t defer_shard_cap;     // > 0: defer_list / defer_count sharded like the heavy list (stage 0)
     // histories over the stage's node budget go to heavy_list (searched
     // again from the root by the heavy stage); null = no stage budget
     uint32_t* heavy_list;

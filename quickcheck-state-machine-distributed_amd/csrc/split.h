@@ -855,10 +855,15 @@ __device__ __forceinline__ void finish_call(const SplitArgs& p, int lane) {
         for (int k = 0; k < T_N; ++k) t = lane == k ? v[k] : t;
         reinterpret_cast<unsigned long long*>(p.totals)[lane] = t;
     }
-    // (stage 0's heavy list: the sum of its shard counters)
+    // (stage 0's heavy and deferred lists: the sums of their shard counters)
     const uint64_t heavy32 = wave_sum64(p.shards && lane < (int)kShards ? p.shards[lane * kShardStride] : 0u);
+    const uint64_t defer = wave_sum64(p.shards && lane < (int)kShards ? p.shards[lane * kShardStride + kDeferShardWord]
+                                                                        : 0u);
     if (p.probe_host && lane <= (int)C_TIMED)
-        p.probe_host[lane] = lane == (int)C_HEAVY32 && p.shards ? (uint32_t)heavy32 : p.cnt[lane];
+        p.probe_host[lane] = !p.shards ? p.cnt[lane]
+                           : lane == (int)C_HEAVY32 ? (uint32_t)heavy32
+                           : lane == (int)C_DEFER   ? (uint32_t)defer + p.cnt[C_DEFER]
+                                                    : p.cnt[lane];
     if (p.probe_host && lane == kProbeWide) p.probe_host[kProbeWide] = p.cnt[C_WIDE];
     if (p.probe_host && lane == kProbeBudget) p.probe_host[kProbeBudget] = p.probe_budget;
     if (p.probe_host && lane == kProbeN) p.probe_host[kProbeN] = (uint32_t)p.s.n_hist;
@@ -870,7 +875,10 @@ __device__ __forceinline__ void finish_call(const SplitArgs& p, int lane) {
         if (p.early) xb[i] = 0ull;
     }
     if (lane < (int)C_N) p.cnt[lane] = lane == (int)C_FIRST_FAIL ? 0xFFFFFFFFu : 0u;
-    if (p.shards && lane < (int)kShards) p.shards[lane * kShardStride] = 0u;
+    if (p.shards && lane < (int)kShards) {
+        p.shards[lane * kShardStride] = 0u;
+        p.shards[lane * kShardStride + kDeferShardWord] = 0u;
+    }
 }
 
 }  // namespace
