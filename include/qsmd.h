@@ -224,7 +224,9 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
 /* Tuning knobs by name (none changes a result):
  *   "stage0_budget"     as qsmd_set_stage0_budget
  *   "stage0_budget_auto" 1: the automatic stage-0 budget (the default)
- *   "stage0w_budget"    the same for 33..64-event histories (default 32)
+ *   "stage0w_budget"    the same for 33..64-event histories (default: automatic,
+ *                       24 when the heavy stage runs in lane mode, 48 in
+ *                       wave mode; "stage0w_budget_auto" 1 restores it)
  *   "stage0_grid"       as qsmd_set_stage0_grid
  *   "split_budget"      as qsmd_set_split_budget
  *   "split_xmemo"       1 (default): the giant stage's exact-count memo
@@ -297,8 +299,9 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *                       workgroup that gave up waiting is BUDGET) */
 int qsmd_set_param(qsmd_ctx* ctx, const char* name, uint64_t value);
 
-/* Read a knob ("stage0_budget": 0 while automatic, "fold", "heavy_mode",
- * "memo_after", "resume_cap", "tail_cap", "tail_min") or "stage0_budget_last": the stage-0 budget the most recent
+/* Read a knob ("stage0_budget": 0 while automatic, "stage0w_budget_auto", "fold",
+ * "heavy_mode", "memo_after", "resume_cap", "tail_cap", "tail_min", "heavy_buckets") or
+ * "stage0_budget_last": the stage-0 budget the most recent
  * finished check call ran with (the automatic one included; waits for the
  * context's last call). */
 int qsmd_get_param(qsmd_ctx* ctx, const char* name, uint64_t* out);

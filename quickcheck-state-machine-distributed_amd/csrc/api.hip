@@ -83,7 +83,13 @@ struct qsmd_ctx {
     // fraction at 16 is far above the threshold; 24 vs 32 with the ordered
     // groups and the tail launch: 1.55 vs 1.49e9, profiles/r06/xbudget)
     bool s0_auto = true;
-    uint64_t stage0w_budget = 32;      // stage-0w node budget before the heavy stage
+    uint64_t stage0w_budget = 32;      // stage-0w node budget before the heavy stage (when not automatic)
+    // automatic stage-0w budget (until one is set): 24 when the heavy stage
+    // runs in lane mode, 48 in wave mode -- config 5 (100k 6x24, 3 calls in
+    // flight): lane mode 9.0 / 11.2 / 10.6 / 9.6e8 at 16 / 24 / 32 / 48, wave
+    // mode 7.4 / 10.7 / 10.1 / 9.2e8 at 32 / 48 / 64 / 96, and its lone call
+    // shortest in wave mode at 48 (profiles/r06/config5/)
+    bool s0w_auto = true;
     uint64_t split_budget = 1024;      // giant stage: whole-search iterations = 16x, heavy-stage cap = 64x
     uint64_t wave_grid = 0;            // heavy stage, wave mode: workgroups (0 = from the last call's heavy count)
     uint64_t wave_min_rem = 4;         // heavy stage, wave mode: nodes with at most this many events left skip the memo
@@ -416,6 +422,10 @@ int qsmd_set_param(qsmd_ctx* c, const char* name, uint64_t value) {
         c->s0_auto = value != 0;
     } else if (n == "stage0w_budget") {
         c->stage0w_budget = value;
+        c->s0w_auto = false;
+    } else if (n == "stage0w_budget_auto") {
+        if (value > 1) return fail(c, QSMD_ERR_ARG, "stage0w_budget_auto: 0 or 1");
+        c->s0w_auto = value != 0;
     } else if (n == "stage0_grid") {
         if (value == 0 || value > 0x7FFFFFFFull) return fail(c, QSMD_ERR_ARG, "bad grid");
         c->stage0_max_grid = value;
@@ -865,7 +875,8 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
     aw.defer_count = cnt + C_WIDE;
     aw.heavy_list = h64;
     aw.heavy_count = cnt + C_HEAVY64;
-    aw.stage0_budget = c->stage0w_budget ? c->stage0w_budget : ~0ull;
+    const uint64_t budget0w = c->s0w_auto ? (lane ? 24u : 48u) : c->stage0w_budget;
+    aw.stage0_budget = budget0w ? budget0w : ~0ull;
     if (!(route & kSkip0w) && !fold)
         HIP_TRY(c, launch_compact64(aw, (uint32_t)((route & kSkip0) ? std::min<uint64_t>(n_groups, kStage0wGrid)
                                                                     : (hint[0] == 0u ? 8u   // (last call: none)
@@ -1243,6 +1254,8 @@ int qsmd_get_param(qsmd_ctx* c, const char* name, uint64_t* out) {
         *out = c->probe_host[kProbeBudget];
     } else if (n == "stage0_budget") {       // the set budget, 0 while automatic
         *out = c->s0_auto ? 0 : c->stage0_budget;
+    } else if (n == "stage0w_budget_auto") {
+        *out = c->s0w_auto ? 1u : 0u;
     } else if (n == "resume_cap") {
         *out = c->resume_cap;
     } else if (n == "fold") {

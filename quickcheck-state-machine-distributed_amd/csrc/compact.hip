@@ -100,7 +100,7 @@ __device__ __forceinline__ int stage_fresh(const SearchArgs& a, bool fresh, uint
     const bool defer = enc_ok && (!small || (s.ok && !s.fits));
     // -> the next stage (stage 0: the group's shard, as the heavy list's --
     // one counter for the batch serialised a wide batch's appends)
-    if (a.defer_shard_cap)
+    if constexpr (G::EV == 32)
         wave_append(defer, h, a.defer_list + (uint64_t)shard * a.defer_shard_cap,
                     a.defer_count + shard * kShardStride, lane);
     else
@@ -125,7 +125,9 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
     __shared__ int32_t s_bal[BANK ? QSMD_BANK_MAX_ACCOUNTS : 1][C_LANES];
 
     const int lane = threadIdx.x;
-    const uint64_t total = a.list ? (uint64_t)list_total(a.list_count, a.list_shard_cap) : a.n_hist;
+    // (stage 0 runs over the whole batch; stage 0w over stage 0's sharded
+    // deferred list, or the whole batch when stage 0 did not run)
+    const uint64_t total = G::EV == 32 || !a.list ? a.n_hist : (uint64_t)list_total(a.list_count, a.list_shard_cap);
     if ((uint64_t)blockIdx.x * C_LANES >= total) return;   // (stage 0w of a call that deferred nothing)
     WaveCounters cnt;
     const uint64_t t0 = a.time_limit ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -137,7 +139,8 @@ __global__ __launch_bounds__(C_LANES, G::EV == 32 ? 4 : 2) void compact_search(S
     for (uint64_t base = (uint64_t)blockIdx.x * C_LANES; base < total; base += (uint64_t)gridDim.x * C_LANES) {
         const uint64_t idx = base + lane;
         const bool active = idx < total;
-        const uint32_t h = active ? (a.list ? list_at(a.list, a.list_count, a.list_shard_cap, idx) : (uint32_t)idx) : 0u;
+        const uint32_t h = !active ? 0u
+                         : G::EV == 32 || !a.list ? (uint32_t)idx : list_at(a.list, a.list_count, a.list_shard_cap, idx);
         const uint32_t shard = (uint32_t)((base / C_LANES) % kShards);
         qsmd_hdr H;
         LaneDFS<MODEL, G> dfs;

@@ -144,7 +144,8 @@ def test_random_any_shape(ctx, model):
     _compare(ctx, m.model_id, b.hdr, b.events, max_nodes=200000)
 
 
-DEFAULTS = {"stage0_budget": 32, "memo_after": 32, "stage0_grid": 65536, "stage0w_budget": 32, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
+DEFAULTS = {"stage0_budget": 32, "memo_after": 32, "stage0_grid": 65536, "stage0w_budget": 32,
+            "stage0w_budget_auto": 1, "heavy_mode": 2, "wave_max": 16384, "wave_min_rem": 4,
             "wave_grid": 0, "split_budget": 1024, "memo_lane_entries": 128, "memo_grid": 0, "split_xmemo": 1,
             "memo_lds": 1, "memo_lds_entries": 64, "dag_states": 128, "memo_lds_cap": 0, "fold": 1, "resume_cap": 0,
             "tail_cap": 256, "tail_min": 65536, "heavy_buckets": 1}
@@ -961,6 +962,24 @@ def test_packed_lookalike_layouts(ctx):
     mixed = codec.encode(models.BANK, hs)
     assert len(mixed.events) == 32 * len(mixed.hdr)
     _compare(ctx, models.MODEL_BANK, mixed.hdr, mixed.events, max_nodes=10**7)
+
+
+def test_stage0w_budget_auto(ctx, knobs):
+    """The automatic stage-0w budget (the default until one is set): 24 with
+    the heavy stage in lane mode, 48 in wave mode; setting "stage0w_budget"
+    turns it off and "stage0w_budget_auto" 1 back on.  Config-5-shaped
+    batches (6x24 Bank, every history 48 events) in both modes and at a set
+    budget: the oracle's results."""
+    assert ctx.get_param("stage0w_budget_auto") == 1
+    hdr, ev, _ = gen.generate_config("bank_6x24", 5, 4000)
+    for heavy in (1, 0):
+        knobs(heavy_mode=heavy)
+        _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**7)
+    knobs(stage0w_budget=40)
+    assert ctx.get_param("stage0w_budget_auto") == 0
+    _compare(ctx, models.MODEL_BANK, hdr, ev, max_nodes=10**7)
+    knobs(stage0w_budget_auto=1)
+    assert ctx.get_param("stage0w_budget_auto") == 1
 
 
 def test_stage0_budget_last():
