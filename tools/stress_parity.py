@@ -24,14 +24,16 @@ import histgen  # noqa: E402
 import oracle_c  # noqa: E402
 from qsmd import codec, device, gen, models  # noqa: E402
 
-KNOBS = {"stage0_budget": [0, 4, 16, 32, 40, 64], "stage0w_budget": [0, 4, 32], "heavy_mode": [0, 1, 2],
+KNOBS = {"stage0_budget": [0, 4, 16, 32, 40, 64], "stage0w_budget": [0, 4, 32], "stage0w_budget_auto": [0, 1],
+         "heavy_mode": [0, 1, 2],
          "split_budget": [1, 16, 64, 1024], "memo_lane_entries": [2, 256], "wave_grid": [0, 5],
          "wave_min_rem": [0, 4, 64], "split_xmemo": [0, 1], "memo_lds": [0, 1, 2], "dag_states": [0, 6, 128, 1024],
          "stage0_budget_auto": [0, 1], "memo_after": [1, 32, 100], "timing_events": [0, 1],
          "fold": [0, 1], "resume_cap": [0, 1, 7, 64],
          "tail_cap": [0, 3, 40, 256], "tail_min": [0, 65536], "heavy_buckets": [0, 1],
          "early": [0, 0, 0, 1]}   # (early: QSMD_FLAG_EARLY_EXIT_BATCH for the batch, not a context knob)
-DEFAULT_KNOBS = {"stage0_budget": 32, "stage0w_budget": 32, "heavy_mode": 2, "split_budget": 1024,
+DEFAULT_KNOBS = {"stage0_budget": 32, "stage0w_budget": 32, "stage0w_budget_auto": 1, "heavy_mode": 2,
+                 "split_budget": 1024,
                  "memo_lane_entries": 128, "wave_grid": 0, "wave_min_rem": 4, "split_xmemo": 1,
                  "memo_lds": 1, "dag_states": 128, "stage0_budget_auto": 1, "memo_after": 32, "timing_events": 0,
                  "fold": 1, "resume_cap": 0, "tail_cap": 256, "tail_min": 65536, "heavy_buckets": 1}
