@@ -230,13 +230,15 @@ int qsmd_set_stage0_budget(qsmd_ctx* ctx, uint64_t nodes);
  *   "stage0_grid"       as qsmd_set_stage0_grid
  *   "split_budget"      as qsmd_set_split_budget
  *   "split_xmemo"       1 (default): the giant stage's exact-count memo
- *   "heavy_mode"        2 (default): the heavy stage in wave mode (one
- *                       wavefront per history, the DFS in wave-uniform
- *                       registers, an LDS memo per wavefront) unless the last
- *                       finished call sent more than "wave_max" (default
- *                       16384) histories there, then lane mode (one lane per
- *                       history, a private memo table per lane); 0: always
- *                       wave mode; 1: always lane mode
+ *   "heavy_mode"        2 (default): the heavy stage in lane mode (one lane
+ *                       per history, a private memo table per lane) when the
+ *                       last finished call sent more than "wave_max"
+ *                       (default 16384) histories there, or sent under a
+ *                       fifth of its batch and had no wide (65..128-event)
+ *                       history; else wave mode (one wavefront per history,
+ *                       the state DAG or the DFS in wave-uniform registers,
+ *                       an LDS memo per wavefront); 0: always wave mode; 1:
+ *                       always lane mode
  *   "memo_lds"          lane mode's memo tables: 1 (default) in LDS when the
  *                       last finished call's heavy histories fit one
  *                       workgroup per CU, else in HBM; 0: always HBM (an

@@ -681,10 +681,22 @@ static int check_device_locked(qsmd_ctx* c, uint32_t model_id, const qsmd_hdr* h
         hint[1] = std::max<uint32_t>(hint[1], (uint32_t)std::min<uint64_t>(n_hist / 4, 0xFFFFFFFEull));
     // heavy-stage mode: lane mode (64 searches per wavefront instruction) for
     // a long heavy list, wave mode (one search per wavefront, its DFS chain
-    // ~10x shorter) for a short one -- by the last finished call's count
+    // ~10x shorter) for a short one -- by the last finished call's count;
+    // and lane mode for a list of short searches of any length: one where
+    // under a fifth of the batch went on (configs 1, 2, 5's shape; one call
+    // at a time lane mode took config 2 on 300 / 2k / 100k / 1M histories at
+    // budget 20 in 0.049 / 0.070 / 0.100 / 0.195 ms against wave mode's
+    // 0.092 / 0.094 / 0.113 / 0.485, config 1 6.9 vs 5.7e9), not a
+    // bug-laden batch's (config 3 on 10k: wave mode 0.128 against 0.48 ms --
+    // the longest of a few thousand long searches), nor one with wide
+    // histories (lane mode hands those to the giant stage);
+    // profiles/r06/wavemax/
     const uint64_t heavy_hint = c->probe_valid ? (uint64_t)hint[1] + hint[2] : 0ull;
+    const bool short_searches = c->probe_valid && heavy_hint > 0 && 5ull * heavy_hint < hint[kProbeN] &&
+                                hint[kProbeWide] == 0u;
     if (c->heavy_mode == 1) route &= ~kSkip0w;   // (lane mode forced: the wide list goes on to the giant stage)
-    bool lane = !(route & kSkip0w) && (c->heavy_mode == 1 || (c->heavy_mode == 2 && heavy_hint > c->wave_max));
+    bool lane = !(route & kSkip0w) &&
+                (c->heavy_mode == 1 || (c->heavy_mode == 2 && (heavy_hint > c->wave_max || short_searches)));
     // lane mode's memo tables in LDS (one wavefront per CU) when the last
     // call's heavy groups fit the CUs, else in HBM (one table per lane slot)
     const bool wide = hint[2] != 0u;   // G64 groups in the launch only when the last call had some

@@ -449,15 +449,20 @@ def test_heavy_any_shape(ctx, knobs, model, heavy, dag):
         _compare(ctx, m.model_id, b.hdr, b.events, models.TicketModel(1, 0, 3), max_nodes=200000)
 
 
-def test_heavy_mode_auto_switches(ctx, knobs):
+@pytest.mark.parametrize("wave_max", [1000, 16384])
+def test_heavy_mode_auto_switches(ctx, knobs, wave_max):
     """heavy_mode 2 (the default) picks wave or lane mode from the routing of
-    the last finished call (lane mode past wave_max heavy histories);
-    results are exact whichever it picks and across the switches (bug-heavy
-    batch, a clean one, the bug-heavy again)."""
-    knobs(heavy_mode=2, wave_max=1000)
+    the last finished call (lane mode past wave_max heavy histories, or for
+    a list under a fifth of the batch; wave mode for a short bug-laden
+    list); results are exact whichever it picks and across the switches
+    (bug-heavy batch, a clean one, the bug-heavy again, a small clean one,
+    one with wide histories)."""
+    knobs(heavy_mode=2, wave_max=wave_max)
     b3 = gen.generate_config("bank_4x16_bugs", 11, 30000)
     b2 = gen.generate_config("bank_4x16", 11, 30000)
-    for hdr, ev, _ in (b3, b3, b3, b2, b2, b3):
+    b2s = gen.generate_config("bank_4x16", 12, 300)
+    b5 = gen.generate_config("bank_6x24", 11, 3000)
+    for hdr, ev, _ in (b3, b3, b3, b2, b2, b3, b2s, b2s, b5, b2, b5):
         _compare(ctx, models.MODEL_BANK, hdr, ev)
 
 
