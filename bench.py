@@ -768,16 +768,18 @@ def main():
                    "clients": cfg["n_clients"], "ops": cfg["n_ops"],
                    "events_per_history": 2 * cfg["n_ops"], "parallelism": f"shard{world}", "calls_in_flight": S,
                    "stage0_budget": budget0 if budget0 >= 0 else "library default",
-                   "heavy_stage": ("lane mode, HBM memo tables" if S > 1 else "library default (wave mode for a "
-                                   "short heavy list)") if not args.param else "knobs: " + ",".join(args.param),
+                   "heavy_stage": ("lane mode, HBM memo tables" if S > 1 else "library default (lane or wave "
+                                   "mode from the last call's heavy list)")
+                   if not args.param else "knobs: " + ",".join(args.param),
                    "counters": {"rccl": "summed on the device, one RCCL all-reduce inside the window",
                                 "rccl-after": "summed on the device, one RCCL all-reduce after the window (the "
                                               "communicator created then): the headline excludes it, exchange_ms "
                                               "times it",
                                 "gloo": "summed on the device, one host (gloo) all-reduce after the window: the "
                                         "headline excludes it, exchange_ms times it"}.get(run.counters)
-                   if use_dist else None,
-                   "exchange_ms": run.exchange_ms if use_dist else None,
+                   if use_dist else "summed on the device after the window: the headline excludes it, "
+                                    "exchange_ms times it",
+                   "exchange_ms": run.exchange_ms,
                    "batches": args.rotate, "fold": fold,
                    "mode": "memo" if args.memo else "exhaustive"},
         "nodes_per_sec": nodes_total / elapsed,
