@@ -288,6 +288,33 @@ LANE_CASES = [("bank_4x16_bugs", 50000, 64, 0),("bank_4x16_bugs", 20000, 8, 300)
               ("ticket_2x10", 20000, 4, 0), ("bank_6x24", 20000, 16, 0), ("bank_6x24", 20000, 8, 500)]
 
 
+@pytest.mark.parametrize("name,n,budget", [("bank_4x16", 60000, 12), ("bank_4x16_bugs", 20000, 20),
+                                           ("bank_6x24", 20000, 12)])
+def test_lane_mode_fold_consistent(ctx, knobs, name, n, budget):
+    """Lane mode keeps the memo slot's balance fold in registers
+    (LaneDFS::fold, updated by undo / try_next); the diagnostic build of the
+    heavy stage (memo_stats_ptr) checks it against the balances in LDS after
+    every try and counts the wavefront iterations where any lane's differs
+    (stats word 12): 0, with the oracle's results."""
+    torch = pytest.importorskip("torch")
+    knobs(heavy_mode=1, memo_lds=0, memo_after=1, stage0_budget=budget, stage0w_budget=budget)
+    hdr, ev, _ = gen.generate_config(name, 17, n)
+    ctx.check_arrays(gen.CONFIGS[name]["model_id"], hdr, ev)   # (the launch's shape follows the last call's lists)
+    groups = (n + 63) // 64
+    stats = torch.zeros(groups * 16, dtype=torch.int64, device="cuda:0")
+    ctx.set_param("memo_stats_groups", groups)
+    ctx.set_param("memo_stats_ptr", stats.data_ptr())
+    try:
+        _compare(ctx, gen.CONFIGS[name]["model_id"], hdr, ev, max_nodes=10**7)
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_param("memo_stats_ptr", 0)
+    q = stats.view(groups, 16).cpu().numpy()
+    q = q[q[:, 6] > 0]
+    assert len(q) > 0 and int(q[:, 15].sum()) > 0        # the heavy stage ran, its iterations counted
+    assert int(q[:, 12].sum()) == 0
+
+
 @pytest.mark.parametrize("name,n,budget,max_nodes", LANE_CASES)
 @pytest.mark.parametrize("entries", [128, 2])
 @pytest.mark.parametrize("lds,lds_entries", [(0, 64), (2, 64), (2, 16), (2, 4)])
