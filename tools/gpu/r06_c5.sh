@@ -5,7 +5,7 @@
 set -o pipefail
 export PYTHONUNBUFFERED=1
 export TMPDIR=/tmp
-O=gpurun_out/r06_c5
+O=gpurun_out/${TAG:-r06_c5}
 mkdir -p $O
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
   python3 bench.py --config bank_6x24 --n-hist 100000 --steps 20 --warmup 3 --inflight 3 --no-extra --no-cpu-baseline --stage0-budget -1 \
